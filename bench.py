@@ -1,0 +1,217 @@
+"""Benchmark: leapfrog steps/s (whole job) + ESS/s of the many-chain Random-trajectory HMC
+on a D=100 unit-MVN target (BASELINE.json metric; configs[1] shape), fp64.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+One step = ONE kernel launch of hmc_random_iters that advances every chain of this GPU by
+--iters-per-step HMC iterations (momentum resample, L ~ U{5..19} leapfrogs, Metropolis test,
+sample stored).  Chains shard over GPUs by global chain id (Philox keyed by it): weak scaling,
+no data-path collective; RCCL is used only for the diagnostics all-reduce after timing.
+Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "understanding-hmc_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
+FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector = FP64 matrix peak (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--chains", type=int, default=131072, help="chains per GPU (8 GPUs -> 1,048,576)")
+    ap.add_argument("--dim", type=int, default=100)
+    ap.add_argument("--iters-per-step", type=int, default=10)
+    ap.add_argument("--fp-mode", default="fast", choices=["fast", "exact"])
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget per process")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ess", action="store_true")
+    return ap.parse_args()
+
+
+# ------------------------------------------------------------------ CPU baseline (oracle port)
+def _cpu_worker(args):
+    seed, D, budget = args
+    os.environ["OMP_NUM_THREADS"] = "1"
+    from oracle import hmc_oracle as O
+    np.random.seed(seed)
+    tgt = O.MVNTarget(np.zeros(D), np.eye(D))
+    core = O.HMCCore(tgt, 0.1)
+    q_start = O.start_pts(np.zeros(D), 2 * np.eye(D), 1)
+    lf = 0
+    t0 = time.time()
+    # rounds of 20 iterations of the reference-equivalent engine until the budget is spent
+    while time.time() - t0 < budget:
+        out = O.gen_sample_random(core, q_start, 1, 20, 0, 1, 5, 20, O.LiveDraws(D, np.eye(D)))
+        lf += out["n_leapfrog"]
+        q_start = out["q_chain"][:, -1, :]
+    return lf, time.time() - t0
+
+
+def cpu_baseline(D, budget):
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    procs = max(1, min(cores, 16))
+    env_threads = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
+    for k in env_threads:
+        os.environ[k] = "1"
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(1000 + i, D, budget) for i in range(procs)])
+    for k, v in env_threads.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+    lf = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    return dict(value=lf / wall, unit="leapfrog steps/s", cores=procs, kind="port",
+                sample=f"oracle/hmc_oracle.py Random engine (reference-equivalent NumPy: eigh logpdf per E, "
+                       f"SVD mvn per draw), D={D} unit MVN, {procs} procs x 1 chain x ~{budget:.0f} s, "
+                       f"{lf} leapfrogs")
+
+
+# ------------------------------------------------------------------ profile-derived HBM traffic
+def pmc_traffic():
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary (profiles/), if present."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from hmc_amd.engine import RandomEngine
+    from hmc_amd.target import MVNTarget
+    from hmc_amd import _lib as H
+    from hmc_amd.diagnostics import convergence_stats
+
+    D, N, S = a.dim, a.chains, a.iters_per_step
+    W, K = a.warmup, a.steps
+    n_iter = (W + K) * S
+    wu = W * S + 1                     # q_chain rows 0..K*S hold exactly the timed iterations
+    tgt = MVNTarget(np.zeros(D), np.eye(D))
+    eng = RandomEngine(tgt, N, n_iter, wu, 1, 5, 20, 0.1, rng="philox", seed=a.seed, fp_mode=a.fp_mode,
+                       chain_offset=rank * N, store_chain=not a.no_ess, device=dev)
+    rs = np.random.RandomState(a.seed + rank)
+    eng.init(torch.as_tensor(rs.standard_normal((N, D)) * np.sqrt(2.0), device=dev))
+    it = 1
+    for _ in range(W):
+        eng.run(it, it + S)
+        it += S
+    torch.cuda.synchronize(dev)
+    c0 = eng.read_counters()
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(K):
+        ev[k][0].record(stream)
+        eng.run(it, it + S)
+        ev[k][1].record(stream)
+        it += S
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    c1 = eng.read_counters()
+    lf_local = int(c1[H.CNT_LEAPFROG] - c0[H.CNT_LEAPFROG])
+    acc = int(c1[H.CNT_ACCEPT] - c0[H.CNT_ACCEPT])
+    tot = torch.tensor([float(lf_local), float(acc), elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        s = tot[:2].clone()
+        dist.all_reduce(s)
+        m = tot[2:].clone()
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        tot = torch.cat([s, m])
+    lf_all, acc_all, t_max, kern_max = tot.cpu().numpy().tolist()
+    value = lf_all / t_max
+    ess = None
+    if not a.no_ess:
+        grp = dist.group.WORLD if world > 1 else None
+        R, neff = convergence_stats(eng.q_chain[:, 1:, :], warm_up_num=0, thin_rate=1, group=grp)
+        ess = dict(ess_per_s_median=float(np.median(neff)) / t_max, ess_per_s_min=float(np.min(neff)) / t_max,
+                   n_eff_median=float(np.median(neff)), rhat_median=float(np.median(R)),
+                   samples_per_chain=K * S)
+
+    if rank == 0:
+        # algorithmic bytes of one launch (S iterations): per chain-iteration one q_chain row +
+        # E + dE (8D + 16 B); per launch q and E_prev are read and written once (16D + 16 B)
+        bytes_launch = N * (S * (8 * D + 16) + 16 * D + 16)
+        lf_launch = lf_local / K
+        # algorithmic flops: 8D per leapfrog + 8D energies per iteration
+        flops_launch = lf_launch * 8 * D + N * S * 8 * D
+        kern_s = kern_ms / 1e3
+        gbs = bytes_launch / kern_s / 1e9
+        tfl = flops_launch / kern_s / 1e12
+        traffic = pmc_traffic()
+        line = {
+            "metric": "leapfrog steps/sec (whole node) + ESS/sec, D=100 MVN",
+            "value": value,
+            "unit": "leapfrog steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": t_max / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (D=100 unit MVN, starts ~ N(0, 2I), Philox4x32-10 draws)",
+            "config": {"workload": f"Random-L HMC, D={D} unit MVN, dt=0.1, L~U{{5..19}}, {N} chains/GPU "
+                                   f"({N * world} total), {S} iterations per step (one fused launch), "
+                                   f"fp_mode={a.fp_mode}",
+                       "chains_per_gpu": N, "dim": D, "iters_per_step": S, "parallelism": f"chains{world}"},
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS,
+                         "traffic": None if traffic is None else traffic.get("bytes_per_launch"),
+                         "kernel": "hmc_random_iters", "kernel_ms": kern_ms,
+                         "bytes_per_launch": bytes_launch},
+            "compute": {"bound": "fp64 vector", "achieved": tfl, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": tfl / FP64_PEAK_TFLOPS, "flops_per_launch": flops_launch},
+            "accept_rate": acc_all / (N * world * K * S),
+            "ess": ess,
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(D, a.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

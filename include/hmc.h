@@ -1,0 +1,194 @@
+/*
+ * hmc.h — C ABI of libhmc.so, the MI355X-native many-chain HMC engine.
+ *
+ * Drop-in boundary for the hot path of jaekor91/understanding-HMC (samplers.py).
+ * The reference has no FFI of its own (pure NumPy); each entry
+ * point below names the reference function whose behaviour it replaces, so a
+ * maintainer can bind it from the reference's Python side with ctypes
+ * (INTEGRATION.md shows the stub).
+ *
+ * Conventions
+ *  - Plain C types only: pointers, sizes, POD structs.  No torch types.
+ *  - Every array argument is a DEVICE pointer (hipMalloc'd or a torch tensor's
+ *    data_ptr()) unless stated otherwise; fp64 throughout; row-major.
+ *  - `stream` is a hipStream_t passed as void* (NULL = default stream).  Calls
+ *    are stream-ordered and asynchronous; the library allocates nothing on the
+ *    hot call and never synchronises the device (graph-capturable).
+ *  - Errors: integer status (hmc_status).  hmc_last_error() returns a message
+ *    for the last failing call on this host thread.  The Python mirror maps
+ *    HMC_EINVAL -> AssertionError (the reference validates with `assert`,
+ *    samplers.py:331-348, :396), HMC_EINDEX -> IndexError (samplers.py:471, Q5),
+ *    HMC_EDMAX -> AssertionError (samplers.py:596-598).
+ */
+#ifndef HMC_AMD_HMC_H
+#define HMC_AMD_HMC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum hmc_status {
+  HMC_OK = 0,
+  HMC_EINVAL = 1,   /* bad argument (reference: AssertionError) */
+  HMC_EDMAX = 2,    /* NUTS doubling exceeded d_max (samplers.py:596-598) */
+  HMC_EHIP = 3,     /* HIP runtime error */
+  HMC_EINDEX = 4,   /* q_chain row out of range during warm-up (samplers.py:471, Q5) */
+  HMC_ENOTSUP = 5   /* shape/feature outside what the kernels support */
+} hmc_status;
+
+enum { HMC_TARGET_DIAG = 0, HMC_TARGET_DENSE = 1 };
+enum { HMC_RNG_REPLAY = 0, HMC_RNG_PHILOX = 1 };
+enum { HMC_MODE_EXACT = 0, HMC_MODE_FAST = 1 };
+
+/* counters[] slots (unsigned long long, device, accumulated with atomics) */
+enum {
+  HMC_CNT_ACCEPT = 0,        /* accepted proposals, i >= warm_up (samplers.py:467)          */
+  HMC_CNT_ACCEPT_WU = 1,     /* accepted proposals, i <  warm_up (samplers.py:469)          */
+  HMC_CNT_LEAPFROG = 2,      /* sum of L actually integrated (the metric's unit of work)     */
+  HMC_CNT_LEAPFROG_SQ = 3,   /* sum of L^2 (reproduces N_total_steps, Q13)                   */
+  HMC_CNT_OOB_REJECT = 4,    /* rejections whose warm-up row index is < -L_chain (Q5)        */
+  HMC_CNT_UNSTABLE = 5,      /* NUTS |E-E0| > 1000 sub-tree rejections (samplers.py:647)     */
+  HMC_CNT_DMAX = 6,          /* NUTS chain-iterations that hit d_max                         */
+  HMC_CNT_ENERGY_EVALS = 7,  /* NUTS energy evaluations (N_total_steps accounting)           */
+  HMC_NCOUNTERS = 8
+};
+
+/* MVN target: V(q) = 0.5*(logdet_const + (q-q0)^T P (q-q0)), dV/dq = P (q-q0).
+ * Replaces the driver closures V/dVdq (case1-script.py:39-49) + utils.normal_lnL
+ * (utils.py:213-218); P = inv(cov0) (case1-script.py:36). */
+typedef struct hmc_target {
+  int32_t D;
+  int32_t kind;            /* HMC_TARGET_DIAG or HMC_TARGET_DENSE                       */
+  const double* q0;        /* [D] mean, NULL => 0                                        */
+  const double* prec;      /* DIAG: [D] diagonal of P, NULL => identity; DENSE: [D*D]    */
+  double logdet_const;     /* D*log(2*pi) + log det(cov0)  (scipy logpdf constant, Q15)  */
+} hmc_target;
+
+/* Kinetic part and integrator step.  Replaces HMC_sampler.cov_p/inv_cov_p/dt
+ * (samplers.py:333, :352-356) as used by K, p_sample and leap_frog (:811-839). */
+typedef struct hmc_kinetic {
+  const double* minv;      /* [D] diagonal of inv(cov_p), NULL => identity (Q3)          */
+  const double* p_scale;   /* [D] sqrt(diag(cov_p)) for in-kernel draws, NULL => 1        */
+  const double* dt_vec;    /* [D] per-dimension step (global_dt=False), NULL => dt        */
+  double dt;               /* scalar step                                                 */
+} hmc_kinetic;
+
+/* Run schedule of gen_sample_random / gen_sample_NUTS (samplers.py:387, :495). */
+typedef struct hmc_schedule {
+  int64_t n_chains;        /* chains handled by this call (this shard)                    */
+  int64_t chain_offset;    /* global id of the first chain: RNG key, so results do not
+                              depend on the number of GPUs or the launch geometry         */
+  int32_t n_iter;          /* Niter                                                        */
+  int32_t warm_up;         /* warm_up_num                                                  */
+  int32_t thin;            /* thin_rate                                                    */
+  int32_t L_chain;         /* 1 + (Niter - warm_up)//thin   (samplers.py:31)              */
+  int32_t L_low, L_high;   /* Random: L ~ U{L_low .. L_high-1} (samplers.py:441, Q1)      */
+  int32_t iter_begin;      /* first iteration i (1-based) of this call                     */
+  int32_t iter_end;        /* one past the last iteration of this call                     */
+  int32_t rng_mode;        /* HMC_RNG_REPLAY or HMC_RNG_PHILOX                             */
+  int32_t fp_mode;         /* HMC_MODE_EXACT (no FMA contraction: bit-identical to the
+                              NumPy reference for diagonal targets) or HMC_MODE_FAST     */
+  int32_t d_max;           /* NUTS max doublings (samplers.py:306, :596)                  */
+  int32_t on_dmax;         /* NUTS: 0 = flag HMC_EDMAX (reference aborts), 1 = count and
+                              keep the current sample                                      */
+  uint64_t seed;           /* Philox4x32-10 key                                             */
+} hmc_schedule;
+
+/* Host-replayed random streams (RNG_REPLAY): the draws the reference would
+ * consume from the global legacy np.random, in its order (Q7). */
+typedef struct hmc_replay {
+  const double* p0;        /* [n_chains][D]        initial momentum (samplers.py:415, Q4) */
+  const double* p;         /* [n_chains][n_iter][D] momentum of iterations 1..Niter (:431) */
+  const int32_t* L;        /* [n_chains][n_iter]    trajectory lengths (:441)              */
+  const double* lnu;       /* [n_chains][n_iter]    log-uniforms (:461)                    */
+  const double* tape;      /* NUTS: [n_chains][tape_stride] directions/uniforms in order  */
+  int64_t tape_stride;
+} hmc_replay;
+
+/* Chain state and outputs (all device).  Result attributes of HMC_sampler
+ * (samplers.py:31-50, :359-360). */
+typedef struct hmc_state {
+  double* q;               /* [n_chains][D] current position (in/out)                     */
+  double* E_prev;          /* [n_chains] E_initial of the previous iteration (Q14)         */
+  double* q_chain;         /* [n_chains][L_chain][D] or NULL (no sample storage)          */
+  double* E_chain;         /* [n_chains][L_chain] or NULL                                  */
+  double* dE_chain;        /* [n_chains][L_chain] or NULL                                  */
+  unsigned long long* counters; /* [HMC_NCOUNTERS]                                          */
+  /* Trajectory capture of global chain 0 for the first n_save iterations (make_movie input;
+   * samplers.py:397-400, :442-475): traj_q[n_save][traj_stride][2] = q[:2] after each step,
+   * traj_len[n_save] = L+1, decision[n_save] = accepted.  NULL / 0 disables capture. */
+  double* traj_q;
+  int32_t* traj_len;
+  int32_t* decision;
+  int32_t n_save;
+  int32_t traj_stride;     /* >= L_high (Random)                                              */
+} hmc_state;
+
+const char* hmc_version(void);
+const char* hmc_last_error(void);
+
+/* Chain initialisation: q_chain[:,0] = q_start, E_chain[:,0] = E(q_start, p0),
+ * dE_chain[:,0] = 0, q = q_start, E_prev = E_chain[:,0].
+ * Replaces samplers.py:413-420 (Random) and :548-555 (NUTS). */
+hmc_status hmc_chain_init(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s,
+                          const hmc_replay* r /* NULL for Philox */, const double* q_start,
+                          hmc_state* st, void* stream);
+
+/* Iterations [iter_begin, iter_end) of the Random-trajectory sampler for all chains:
+ * fused momentum resample -> E0 -> L leapfrogs -> E1 -> Metropolis test -> store.
+ * Replaces HMC_sampler.gen_sample_random, samplers.py:428-475 (+ :811-839). */
+hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s,
+                            const hmc_replay* r /* NULL for Philox */, hmc_state* st, void* stream);
+
+/* Batched single leapfrog step (n independent (p, q) rows).
+ * Replaces HMC_sampler.leap_frog(p_old, q_old), samplers.py:831-839. */
+hmc_status hmc_leapfrog(const hmc_target* t, const hmc_kinetic* k, int64_t n, const double* p,
+                        const double* q, double* p_out, double* q_out, int32_t fp_mode,
+                        void* stream);
+
+/* Batched total energy E(q, p) = V(q) + K(p) of n rows.
+ * Replaces HMC_sampler.E / K (samplers.py:811-823) with V of utils.py:213-218. */
+hmc_status hmc_energy(const hmc_target* t, const hmc_kinetic* k, int64_t n, const double* q,
+                      const double* p, double* E_out, void* stream);
+
+/* The standard normals the Philox mode draws for (chain, iteration): out[n][2*npairs].
+ * Debug/verification entry (statistical tests of the in-kernel generator). */
+hmc_status hmc_rng_normals(uint64_t seed, int64_t chain0, int64_t n, int32_t iteration,
+                           int32_t npairs, double* out, void* stream);
+
+/* Raw Philox4x32-10 blocks: out[n][4] = philox(ctr = {x0 + i, x1, x2, x3}, key). */
+hmc_status hmc_philox(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3, uint32_t k0,
+                      uint32_t k1, int64_t n, uint32_t* out, void* stream);
+
+/* ---------------------------------------------------------------- diagnostics
+ * Split-chain R-hat / ESS building blocks (utils.py:77-179) and the per-dimension
+ * mean/std of plot_samples (samplers.py:213, :246).  Chains are read in place:
+ * element (chain m, sample s, dim d) = x[base + m*chain_stride + s*sample_stride + d].
+ * All sums are deterministic (fixed-order two-stage reductions); `work` is caller-owned
+ * scratch of the size the *_work_size query returns (doubles). */
+
+/* Per split chain j (= 2m + half; half h covers samples [h*n, h*n+n)): mean and std
+ * (ddof=1) of every dimension -> mean_out/std_out [2*n_chains][D].  utils.py:88-119. */
+hmc_status hmc_split_moments(const double* x, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
+                             int64_t base, int32_t n, int32_t D, double* mean_out, double* std_out, void* stream);
+
+/* out[d] = sum over rows (o, i) of x[base + o*outer_stride + i*inner_stride + d], or of
+ * (x - center[d])^2 when center != NULL.  Used for W, B (utils.py:112-120) and mean/std. */
+int64_t hmc_rowsum_work_size(int64_t rows, int32_t D);
+hmc_status hmc_rowsum(const double* x, int64_t n_outer, int64_t outer_stride, int64_t n_inner,
+                      int64_t inner_stride, int64_t base, int32_t D, const double* center, double* work,
+                      double* out, void* stream);
+
+/* Variogram sums out[t - t0][d] = sum_j sum_s (x_j[s+t] - x_j[s])^2 over split chains,
+ * lags t in [t0, t1).  utils.py:161-179 (before its division by m*(n-t)). */
+int64_t hmc_variogram_work_size(int64_t n_chains, int32_t D, int32_t nlags);
+hmc_status hmc_variogram(const double* x, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
+                         int64_t base, int32_t n, int32_t D, int32_t t0, int32_t t1, double* work, double* out,
+                         void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HMC_AMD_HMC_H */

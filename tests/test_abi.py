@@ -1,0 +1,72 @@
+"""C-ABI boundary checks that need no GPU: libhmc.so loads, exports every function
+include/hmc.h declares, and the ctypes struct mirrors match the C layouts."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "hmc.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^[A-Za-z_][\w \*]*?\b(hmc_[a-z_0-9]+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_entry_points():
+    names = _declared()
+    for must in ("hmc_chain_init", "hmc_random_iters", "hmc_leapfrog", "hmc_energy", "hmc_split_moments",
+                 "hmc_variogram", "hmc_rowsum"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from hmc_amd import _lib
+    L = _lib.lib()
+    for name in _declared():
+        assert hasattr(L, name), name
+    assert set(_declared()) == set(_lib.SYMBOLS), "ctypes SYMBOLS out of sync with include/hmc.h"
+    assert L.hmc_version().startswith(b"hmc_amd")
+
+
+def test_struct_layouts():
+    from hmc_amd import _lib as H
+    # sizes follow from the C declarations (x86-64 SysV alignment)
+    assert ctypes.sizeof(H.Target) == 32
+    assert ctypes.sizeof(H.Kinetic) == 32
+    assert ctypes.sizeof(H.Schedule) == 8 + 8 + 12 * 4 + 8
+    assert ctypes.sizeof(H.Replay) == 48
+    assert ctypes.sizeof(H.State) == 9 * 8 + 8
+
+
+def test_invalid_arguments_map_to_reference_exceptions():
+    """Validation runs on the host before any HIP call: the reference's asserts become
+    AssertionError via hmc_status HMC_EINVAL (samplers.py:331-348)."""
+    from hmc_amd import _lib as H
+    L = H.lib()
+    T = H.Target(0, 0, None, None, 0.0)          # D = 0 -> EINVAL
+    K = H.Kinetic(None, None, None, 0.1)
+    S = H.Schedule(4, 0, 10, 0, 1, 11, 5, 20, 1, 11, 1, 0, 10, 0, 0)
+    st = H.State()
+    with pytest.raises(AssertionError):
+        H.check(L.hmc_random_iters(T, K, S, None, st, None), "x")
+    T.D = 3
+    S.L_chain = 7                                 # wrong L_chain
+    with pytest.raises(AssertionError):
+        H.check(L.hmc_random_iters(T, K, S, None, st, None), "x")
+    S.L_chain = 11
+    S.L_high = 5                                  # L_low >= L_high (randint raises)
+    with pytest.raises(AssertionError):
+        H.check(L.hmc_random_iters(T, K, S, None, st, None), "x")
+
+
+def test_no_cpu_fallback_when_library_missing(tmp_path, monkeypatch):
+    import importlib
+    from hmc_amd import _lib as H
+    monkeypatch.setattr(H, "_lib", None)
+    monkeypatch.setattr(H, "LIB_PATH", str(tmp_path / "missing.so"))
+    with pytest.raises(RuntimeError, match="libhmc.so not found"):
+        H.lib()
+    importlib.reload(H)

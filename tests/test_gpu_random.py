@@ -1,0 +1,210 @@
+"""GPU parity of the Random-trajectory engine (hmc_random_iters) against the reference.
+
+Replay mode feeds the kernels the exact draws the reference consumed (golden
+fixtures recorded from the reference itself, tests/golden/make_golden.py), so:
+  * diagonal targets, fp_mode="exact": q_chain BIT-EXACT, acceptance counts,
+    N_total_steps and the chain-0 trajectory capture exact; E_chain within 1e-12
+    relative (energy sums are re-associated vs scipy's eigh-based logpdf);
+  * fp_mode="fast" (FMA-contracted integrator): q_chain within 1e-9 relative,
+    identical accept decisions on these fixtures.
+Philox mode at BASELINE sizes is checked through size-independent properties
+(determinism, shard invariance, moments, acceptance).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from oracle import hmc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DIAG_FIXTURES = ["f1_case1a.npz", "f2_case1c_small.npz", "f8_diag_thin_vecdt.npz", "f9_wu0_thin2.npz",
+                 "f10_case2a.npz"]
+
+
+def _sampler_from_golden(g, **kw):
+    from hmc_amd.samplers import HMC_sampler
+    from hmc_amd.target import MVNTarget
+    m = g["meta"]
+    dt = g["dt"]
+    dt = float(dt) if dt.ndim == 0 else dt
+    tgt = O.MVNTarget(g["q0"], g["cov0"])
+    # explicit target: exact q0 / inv(cov0) as the reference computed them (probing is exact only for q0 = 0)
+    return HMC_sampler(m["D"], tgt.V, tgt.dVdq, Nchain=m["Nchain"], Niter=m["Niter"], sampler_type="Random",
+                       L_low=m["L_low"], L_high=m["L_high"], dt=dt, thin_rate=m["thin"], warm_up_num=m["warm_up"],
+                       cov_p=g["cov_p"], target=MVNTarget(g["q0"], g["cov0"]), **kw)
+
+
+def _run_replay(g, fp_mode="exact"):
+    """Run the product in replay mode on the recorded streams: the live global RNG is
+    re-seeded and re-advanced past start_pts exactly as in the reference run."""
+    m = g["meta"]
+    h = _sampler_from_golden(g, fp_mode=fp_mode)
+    np.random.seed(m["seed"])
+    np.random.multivariate_normal(np.zeros(m["D"]), np.diag(np.ones(m["D"])) * m["start_scale"], size=m["Nchain"])
+    h.gen_sample(g["q_start"], N_save_chain0=m["n_save"], verbose=False)
+    return h
+
+
+@pytest.mark.parametrize("fx", DIAG_FIXTURES)
+def test_replay_exact_matches_reference(fx):
+    g = load_golden(fx)
+    m = g["meta"]
+    h = _run_replay(g, "exact")
+    assert np.array_equal(h.q_chain, g["q_chain"]), "q_chain not bit-identical to the reference"
+    np.testing.assert_allclose(h.E_chain[:, :, 0], g["E_chain"], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(h.dE_chain[:, :, 0], g["dE_chain"], rtol=1e-9, atol=1e-11)
+    assert h.accept_R == float(g["accept_R"])
+    if m["warm_up"] > 0:
+        assert h.accept_R_warm_up == float(g["accept_R_warm_up"])
+    assert h.N_total_steps == int(g["N_total_steps"])
+    assert h.n_leapfrog == int(g["n_leapfrog"])
+    if m["n_save"]:
+        assert np.array_equal(h.decision_chain[:, 0], g["decision_chain"])
+        assert np.array_equal(np.concatenate(h.phi_q), g["phi_q_flat"])
+
+
+@pytest.mark.parametrize("fx", DIAG_FIXTURES)
+def test_replay_fast_within_tolerance(fx):
+    g = load_golden(fx)
+    h = _run_replay(g, "fast")
+    np.testing.assert_allclose(h.q_chain, g["q_chain"], rtol=1e-9, atol=1e-9)
+    assert h.accept_R == float(g["accept_R"])
+
+
+@pytest.mark.parametrize("fx", ["f1_case1a.npz", "f2_case1c_small.npz", "f9_wu0_thin2.npz"])
+def test_convergence_stats_on_device(fx):
+    """R-hat / ESS / per-dim mean,std computed by the diagnostics kernels vs the reference
+    values (north_star tolerance 1e-6 rel; observed ~1e-13)."""
+    g = load_golden(fx)
+    h = _run_replay(g, "exact")
+    h.compute_convergence_stats()
+    np.testing.assert_allclose(h.R_q, g["R_q"], rtol=1e-10)
+    np.testing.assert_allclose(h.n_eff_q, g["n_eff_q"], rtol=1e-8)
+    from hmc_amd.diagnostics import per_dim_mean_std
+    mean, std = per_dim_mean_std(h.q_chain_device)
+    np.testing.assert_allclose(mean, g["mean"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(std, g["std"], rtol=1e-10)
+
+
+def test_convergence_stats_vectors_device():
+    """utils.convergence_stats on the reference's synthetic AR(1) vectors (incl. thinning,
+    warm-up offsets, odd lengths)."""
+    from hmc_amd.diagnostics import convergence_stats
+    g = load_golden("f5_convergence.npz")
+    for tag in "abcdf":
+        x = g[f"{tag}_x"]
+        R, neff = convergence_stats(x, warm_up_num=0, thin_rate=1)
+        np.testing.assert_allclose(R, g[f"{tag}_R"], rtol=1e-10)
+        np.testing.assert_allclose(neff, g[f"{tag}_neff"], rtol=1e-8)
+        R5, neff5 = convergence_stats(x, thin_rate=5, warm_up_num=3)
+        np.testing.assert_allclose(R5, g[f"{tag}_R_thin5"], rtol=1e-10)
+        np.testing.assert_allclose(neff5, g[f"{tag}_neff_thin5"], rtol=1e-8)
+
+
+def test_leapfrog_and_energy_vectors():
+    """Batched leap_frog / E (samplers.py:811-839) vs the reference's single-call outputs."""
+    g = load_golden("f4_leapfrog.npz")
+    for tag, exact in (("unit100", True), ("diag10_vecdt", True), ("dense100", False)):
+        from hmc_amd.samplers import HMC_sampler
+        tgt = O.MVNTarget(g[f"{tag}_q0"], g[f"{tag}_cov0"])
+        dt = g[f"{tag}_dt"]
+        from hmc_amd.target import MVNTarget
+        h = HMC_sampler(tgt.q0.size, tgt.V, tgt.dVdq, Nchain=2, Niter=1, sampler_type="Random", L_low=1,
+                        L_high=2, dt=float(dt) if dt.ndim == 0 else dt, cov_p=g[f"{tag}_cov_p"],
+                        target=MVNTarget(g[f"{tag}_q0"], g[f"{tag}_cov0"]))
+        pn, qn = h.leap_frog(g[f"{tag}_p"], g[f"{tag}_q"])
+        if exact:
+            assert np.array_equal(pn, g[f"{tag}_pn"]) and np.array_equal(qn, g[f"{tag}_qn"])
+        else:  # dense BLAS dgemv summation order is unspecified
+            np.testing.assert_allclose(pn, g[f"{tag}_pn"], rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(qn, g[f"{tag}_qn"], rtol=1e-13, atol=1e-13)
+        E = h.E(g[f"{tag}_q"], g[f"{tag}_p"])
+        np.testing.assert_allclose(E, g[f"{tag}_E"], rtol=1e-12)
+
+
+def test_philox_known_answers():
+    """Random123 Philox4x32-10 known-answer vectors."""
+    from hmc_amd import _lib as H
+    L = H.lib()
+    out = torch.zeros(4, dtype=torch.int32, device="cuda")
+    kats = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+            ((0xffffffff,) * 4, (0xffffffff,) * 2, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+            ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+             (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for ctr, key, want in kats:
+        H.check(L.hmc_philox(*ctr, *key, 1, out.data_ptr(), None))
+        got = tuple(int(v) & 0xffffffff for v in out.cpu().numpy())
+        assert got == want
+
+
+def test_philox_normals_moments():
+    from hmc_amd import _lib as H
+    L = H.lib()
+    n, npairs = 1 << 16, 8
+    out = torch.empty((n, 2 * npairs), dtype=torch.float64, device="cuda")
+    H.check(L.hmc_rng_normals(7, 0, n, 3, npairs, out.data_ptr(), None))
+    z = out.cpu().numpy().ravel()
+    N = z.size
+    assert abs(z.mean()) < 5 / np.sqrt(N)
+    assert abs(z.var() - 1) < 5 * np.sqrt(2 / N)
+    assert abs(np.mean(z ** 3)) < 5 * np.sqrt(15 / N)
+    assert abs(np.mean(z ** 4) - 3) < 5 * np.sqrt(96 / N)
+    # independent streams: correlation between the two normals of a pair and across chains
+    assert abs(np.corrcoef(out[:, 0].cpu(), out[:, 1].cpu())[0, 1]) < 5 / np.sqrt(n)
+    assert abs(np.corrcoef(out[:-1, 0].cpu(), out[1:, 0].cpu())[0, 1]) < 5 / np.sqrt(n)
+
+
+def _philox_run(N, D, Niter, wu, seed=1, offset=0, fp_mode="fast", target=None, ipl=None):
+    from hmc_amd.samplers import HMC_sampler
+    from hmc_amd.target import MVNTarget
+    t = target or MVNTarget(np.zeros(D), np.eye(D))
+    h = HMC_sampler(D, None, None, Nchain=N, Niter=Niter, sampler_type="Random", L_low=5, L_high=20, dt=0.1,
+                    warm_up_num=wu, target=t, rng="philox", seed=seed, fp_mode=fp_mode, chain_offset=offset,
+                    iters_per_launch=ipl)
+    rs = np.random.RandomState(seed + 1000 + offset)
+    q0 = rs.standard_normal((N, D)) * np.sqrt(2)
+    h.gen_sample(q0, verbose=False)
+    return h, q0
+
+
+def test_philox_deterministic_and_shard_invariant():
+    """Results are a pure function of (seed, global chain id): identical across runs, launch
+    splits (iters_per_launch) and chain shards (chain_offset), as multi-GPU sharding needs."""
+    N, D = 4096, 100
+    h1, q0 = _philox_run(N, D, 12, 4)
+    h2, _ = _philox_run(N, D, 12, 4, ipl=5)
+    assert np.array_equal(h1.q_chain, h2.q_chain)
+    from hmc_amd.samplers import HMC_sampler
+    from hmc_amd.target import MVNTarget
+    half = N // 2
+    parts = []
+    for off in (0, half):
+        h = HMC_sampler(D, None, None, Nchain=half, Niter=12, sampler_type="Random", L_low=5, L_high=20, dt=0.1,
+                        warm_up_num=4, target=MVNTarget(np.zeros(D), np.eye(D)), rng="philox", seed=1,
+                        fp_mode="fast", chain_offset=off)
+        h.gen_sample(q0[off:off + half], verbose=False)
+        parts.append(h.q_chain)
+    assert np.array_equal(np.concatenate(parts), h1.q_chain)
+
+
+def test_philox_baseline_shape_statistics():
+    """BASELINE config 2 shape (D=100 unit MVN, dt=0.1, L in [5,20)) at 65,536 chains:
+    acceptance ~0.99 (case1c reference: 0.9915), post-warm-up moments of N(0, I)."""
+    N, D = 65536, 100
+    h, _ = _philox_run(N, D, 30, 10)
+    assert 0.985 < h.accept_R < 0.997
+    x = h.q_chain[:, 1:, :]
+    assert np.abs(x.mean(axis=(0, 1))).max() < 0.02
+    assert np.abs(x.std(axis=(0, 1)) - 1).max() < 0.02
+    lf = h.n_leapfrog
+    assert abs(lf / (N * 30) - 12.0) < 0.05          # E[L] = 12 for U{5..19}
+
+
+def test_fp_modes_agree_statistically():
+    N, D = 8192, 100
+    he, _ = _philox_run(N, D, 10, 2, fp_mode="exact")
+    hf, _ = _philox_run(N, D, 10, 2, fp_mode="fast")
+    # same draws, trajectories differ only by FMA rounding: tiny differences everywhere
+    np.testing.assert_allclose(he.q_chain, hf.q_chain, rtol=1e-8, atol=1e-8)

@@ -1,0 +1,243 @@
+// hmc_capi.cpp — extern "C" entry points of libhmc.so (declared in include/hmc.h).
+//
+// Validation mirrors the reference's asserts (samplers.py:331-348, :396) and returns
+// HMC_EINVAL instead of raising; the Python mirror re-raises AssertionError.
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "hmc.h"
+#include "hmc_internal.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+hmc_status fail(hmc_status st, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return st;
+}
+
+hmc_status hip_status(hipError_t e, const char* where) {
+  if (e == hipSuccess) return HMC_OK;
+  return fail(HMC_EHIP, "%s: %s", where, hipGetErrorString(e));
+}
+
+// Python floor division (the reference computes (i - warm_up)//thin with Python ints).
+int64_t floordiv(int64_t a, int64_t b) {
+  int64_t q = a / b;
+  if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
+  return q;
+}
+
+hmc_status check_schedule(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, bool random) {
+  if (!t || !k || !s) return fail(HMC_EINVAL, "null target/kinetic/schedule");
+  if (t->D < 1) return fail(HMC_EINVAL, "D must be >= 1");
+  if (t->kind != HMC_TARGET_DIAG && t->kind != HMC_TARGET_DENSE) return fail(HMC_EINVAL, "bad target kind");
+  if (t->kind == HMC_TARGET_DENSE && !t->prec) return fail(HMC_EINVAL, "dense target needs prec");
+  if (s->n_chains < 0) return fail(HMC_EINVAL, "n_chains < 0");
+  if (s->n_iter < 1 || s->thin < 1 || s->warm_up < 0) return fail(HMC_EINVAL, "bad Niter/thin/warm_up");
+  const int64_t Lc = 1 + floordiv(s->n_iter - s->warm_up, s->thin);  // samplers.py:31
+  if (Lc < 1 || Lc != s->L_chain) return fail(HMC_EINVAL, "L_chain must be 1+(Niter-warm_up)//thin >= 1");
+  if (!(std::isfinite(k->dt)) && !k->dt_vec) return fail(HMC_EINVAL, "dt must be set (samplers.py:332)");
+  if (random && s->L_high <= s->L_low) return fail(HMC_EINVAL, "L_low must be < L_high (randint)");
+  if (random && s->rng_mode == HMC_RNG_PHILOX && s->L_low < 0) return fail(HMC_EINVAL, "L_low < 0");
+  if (s->rng_mode != HMC_RNG_REPLAY && s->rng_mode != HMC_RNG_PHILOX) return fail(HMC_EINVAL, "bad rng_mode");
+  if (s->fp_mode != HMC_MODE_EXACT && s->fp_mode != HMC_MODE_FAST) return fail(HMC_EINVAL, "bad fp_mode");
+  return HMC_OK;
+}
+
+hmc::RandArgs rand_args(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, const hmc_replay* r,
+                        hmc_state* st, const hmc::Layout& lay) {
+  hmc::RandArgs a{};
+  a.n = s->n_chains;
+  a.chain_offset = s->chain_offset;
+  a.D = t->D;
+  a.npairs = lay.npairs;
+  a.lpc = lay.lpc;
+  a.cpw = lay.cpw;
+  a.niter = s->n_iter;
+  a.wu = s->warm_up;
+  a.thin = s->thin;
+  a.Lc = s->L_chain;
+  a.L_low = s->L_low;
+  a.L_high = s->L_high;
+  a.it0 = s->iter_begin;
+  a.it1 = s->iter_end;
+  a.i_oob = (int)(s->warm_up - (int64_t)s->L_chain * s->thin);  // rejections at i < i_oob index < -L_chain
+  a.k0 = (uint32_t)s->seed;
+  a.k1 = (uint32_t)(s->seed >> 32);
+  a.dt = k->dt;
+  a.h = k->dt * 0.5;
+  a.logc = t->logdet_const;
+  a.q0 = t->q0;
+  a.prec = t->prec;
+  a.minv = k->minv;
+  a.pscale = k->p_scale;
+  a.dtv = k->dt_vec;
+  if (r) {
+    a.rp0 = r->p0;
+    a.rp = r->p;
+    a.rlnu = r->lnu;
+    a.rL = r->L;
+  }
+  a.q = st->q;
+  a.Eprev = st->E_prev;
+  a.qc = st->q_chain;
+  a.Ec = st->E_chain;
+  a.dEc = st->dE_chain;
+  a.cnt = st->counters;
+  if (st->traj_q && st->traj_len && st->decision && st->n_save > 0) {
+    a.traj_q = st->traj_q;
+    a.traj_len = st->traj_len;
+    a.decision = st->decision;
+    a.n_save = st->n_save;
+    a.traj_stride = st->traj_stride;
+  }
+  return a;
+}
+
+bool general_diag(const hmc_target* t, const hmc_kinetic* k) {
+  return t->q0 || t->prec || k->minv || k->p_scale || k->dt_vec;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* hmc_version(void) { return "hmc_amd 0.1.0 gfx950 (diag random kernels, C ABI v1)"; }
+
+const char* hmc_last_error(void) { return g_err.c_str(); }
+
+hmc_status hmc_chain_init(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, const hmc_replay* r,
+                          const double* q_start, hmc_state* st, void* stream) {
+  if (hmc_status e = check_schedule(t, k, s, false)) return e;
+  if (!st || !st->q || !st->E_prev || !q_start) return fail(HMC_EINVAL, "null state/q_start");
+  const bool replay = s->rng_mode == HMC_RNG_REPLAY;
+  if (replay && (!r || !r->p0)) return fail(HMC_EINVAL, "replay mode needs p0");
+  if (s->n_chains == 0) return HMC_OK;
+  if (t->kind == HMC_TARGET_DENSE) return fail(HMC_ENOTSUP, "dense target: not in this build");
+  const int L_lo = s->L_high > s->L_low ? s->L_low : 5, L_hi = s->L_high > s->L_low ? s->L_high : 20;
+  const hmc::Layout lay = hmc::choose_layout(t->D, L_lo, L_hi);
+  if (lay.K == 0) return fail(HMC_ENOTSUP, "D=%d too large for the diagonal kernels", t->D);
+  hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
+  a.qstart = q_start;
+  return hip_status(hmc::launch_random_init(a, lay, general_diag(t, k), replay, (hipStream_t)stream),
+                    "hmc_chain_init");
+}
+
+hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, const hmc_replay* r,
+                            hmc_state* st, void* stream) {
+  if (hmc_status e = check_schedule(t, k, s, true)) return e;
+  if (!st || !st->q || !st->E_prev) return fail(HMC_EINVAL, "null state");
+  if (s->iter_begin < 1 || s->iter_end < s->iter_begin || s->iter_end > s->n_iter + 1)
+    return fail(HMC_EINVAL, "iteration range must satisfy 1 <= begin <= end <= Niter+1");
+  const bool replay = s->rng_mode == HMC_RNG_REPLAY;
+  if (replay && (!r || !r->p || !r->L || !r->lnu)) return fail(HMC_EINVAL, "replay mode needs p, L, lnu");
+  if (s->n_chains == 0 || s->iter_end == s->iter_begin) return HMC_OK;
+  if (t->kind == HMC_TARGET_DENSE) return fail(HMC_ENOTSUP, "dense target: not in this build");
+  const hmc::Layout lay = hmc::choose_layout(t->D, s->L_low, s->L_high);
+  if (lay.K == 0) return fail(HMC_ENOTSUP, "D=%d too large for the diagonal kernels", t->D);
+  if (st->n_save > 0 && st->traj_q && st->traj_stride < s->L_high)
+    return fail(HMC_EINVAL, "traj_stride must be >= L_high");
+  const hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
+  return hip_status(hmc::launch_random_iters(a, lay, s->fp_mode == HMC_MODE_EXACT, general_diag(t, k), replay,
+                                             (hipStream_t)stream),
+                    "hmc_random_iters");
+}
+
+hmc_status hmc_leapfrog(const hmc_target* t, const hmc_kinetic* k, int64_t n, const double* p, const double* q,
+                        double* p_out, double* q_out, int32_t fp_mode, void* stream) {
+  if (!t || !k || t->D < 1 || n < 0) return fail(HMC_EINVAL, "bad arguments");
+  if (n > 0 && (!p || !q || !p_out || !q_out)) return fail(HMC_EINVAL, "null row pointers");
+  if (p_out == p || q_out == q || p_out == q || q_out == p) return fail(HMC_EINVAL, "outputs alias inputs");
+  hmc::RowArgs a{};
+  a.n = n;
+  a.D = t->D;
+  a.dense = t->kind == HMC_TARGET_DENSE;
+  a.q0 = t->q0;
+  a.prec = t->prec;
+  a.minv = k->minv;
+  a.dtv = k->dt_vec;
+  a.dt = k->dt;
+  a.logc = t->logdet_const;
+  a.p = p;
+  a.q = q;
+  a.po = p_out;
+  a.qo = q_out;
+  return hip_status(hmc::launch_leapfrog_rows(a, fp_mode == HMC_MODE_EXACT, (hipStream_t)stream), "hmc_leapfrog");
+}
+
+hmc_status hmc_energy(const hmc_target* t, const hmc_kinetic* k, int64_t n, const double* q, const double* p,
+                      double* E_out, void* stream) {
+  if (!t || !k || t->D < 1 || n < 0) return fail(HMC_EINVAL, "bad arguments");
+  if (n > 0 && (!p || !q || !E_out)) return fail(HMC_EINVAL, "null row pointers");
+  hmc::RowArgs a{};
+  a.n = n;
+  a.D = t->D;
+  a.dense = t->kind == HMC_TARGET_DENSE;
+  a.q0 = t->q0;
+  a.prec = t->prec;
+  a.minv = k->minv;
+  a.logc = t->logdet_const;
+  a.p = p;
+  a.q = q;
+  a.E = E_out;
+  return hip_status(hmc::launch_energy_rows(a, (hipStream_t)stream), "hmc_energy");
+}
+
+hmc_status hmc_rng_normals(uint64_t seed, int64_t chain0, int64_t n, int32_t iteration, int32_t npairs, double* out,
+                           void* stream) {
+  if (n < 0 || npairs < 0 || iteration < 0) return fail(HMC_EINVAL, "bad arguments");
+  if (n * npairs > 0 && !out) return fail(HMC_EINVAL, "null out");
+  return hip_status(hmc::launch_rng_normals((uint32_t)seed, (uint32_t)(seed >> 32), chain0, n, iteration, npairs,
+                                            out, (hipStream_t)stream),
+                    "hmc_rng_normals");
+}
+
+hmc_status hmc_philox(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3, uint32_t k0, uint32_t k1, int64_t n,
+                      uint32_t* out, void* stream) {
+  if (n < 0 || (n > 0 && !out)) return fail(HMC_EINVAL, "bad arguments");
+  return hip_status(hmc::launch_philox(make_uint4(x0, x1, x2, x3), k0, k1, n, out, (hipStream_t)stream),
+                    "hmc_philox");
+}
+
+int64_t hmc_rowsum_work_size(int64_t rows, int32_t D) { return hmc::diag_rowsum_work(rows, D); }
+
+int64_t hmc_variogram_work_size(int64_t n_chains, int32_t D, int32_t nlags) {
+  return hmc::diag_variogram_work(n_chains, D, nlags);
+}
+
+hmc_status hmc_split_moments(const double* x, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
+                             int64_t base, int32_t n, int32_t D, double* mean_out, double* std_out, void* stream) {
+  if (!x || !mean_out || !std_out || n_chains < 1 || n < 1 || D < 1) return fail(HMC_EINVAL, "bad arguments");
+  return hip_status(hmc::launch_split_moments(x, n_chains, chain_stride, sample_stride, base, n, D, mean_out,
+                                              std_out, (hipStream_t)stream),
+                    "hmc_split_moments");
+}
+
+hmc_status hmc_rowsum(const double* x, int64_t n_outer, int64_t outer_stride, int64_t n_inner, int64_t inner_stride,
+                      int64_t base, int32_t D, const double* center, double* work, double* out, void* stream) {
+  if (!x || !work || !out || n_outer < 1 || n_inner < 1 || D < 1) return fail(HMC_EINVAL, "bad arguments");
+  return hip_status(hmc::launch_rowsum(x, n_outer, outer_stride, n_inner, inner_stride, base, D, center, work, out,
+                                       (hipStream_t)stream),
+                    "hmc_rowsum");
+}
+
+hmc_status hmc_variogram(const double* x, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
+                         int64_t base, int32_t n, int32_t D, int32_t t0, int32_t t1, double* work, double* out,
+                         void* stream) {
+  if (!x || !work || !out || n_chains < 1 || n < 1 || D < 1 || t0 < 1 || t1 <= t0)
+    return fail(HMC_EINVAL, "bad arguments");
+  return hip_status(hmc::launch_variogram(x, n_chains, chain_stride, sample_stride, base, n, D, t0, t1, work, out,
+                                          (hipStream_t)stream),
+                    "hmc_variogram");
+}
+
+}  // extern "C"

@@ -1,0 +1,180 @@
+// hmc_diag.hip — convergence diagnostics on the device (utils.py:77-179; samplers.py:213, :246).
+//
+// The reference's convergence_stats splits every chain into two halves
+// (utils.py:88-104), then needs, per dimension:
+//   * per split chain j: mean_j and std_j (ddof=1)             -> k_split_moments
+//   * sums over j of std_j, mean_j, (mean_j - mean_all)^2        -> k_rowsum (two-stage, deterministic)
+//   * variogram sums  sum_j sum_s (x_j[s+t] - x_j[s])^2, t = lags -> k_variogram (two-stage)
+// Everything is additive over chains, so on several GPUs each rank reduces its own
+// chains and one small all-reduce combines the per-dimension sums.
+// Chains are read in place through strides: element (chain m, sample s, dim d) sits at
+//   x[base + m*chain_stride + s*sample_stride + d]
+// which covers q_chain[:, 1:, :], warm-up offsets and thinning without copies.
+#include "hmc_device.hpp"
+#include "hmc_internal.hpp"
+
+namespace hmc {
+
+namespace {
+
+constexpr int kRowChunk = 256;   // rows per partial-sum block
+constexpr int kDimTile = 64;     // dims per block (lane = dim: coalesced row reads)
+
+struct Src {
+  const double* x;
+  int64_t chain_stride, sample_stride, base;
+  int64_t n_chains;
+  int n, D;
+};
+
+__device__ __forceinline__ const double* split_ptr(const Src& s, int64_t j, int smp) {
+  const int64_t m = j >> 1;
+  const int h = (int)(j & 1);
+  return s.x + s.base + m * s.chain_stride + (int64_t)(h * s.n + smp) * s.sample_stride;
+}
+
+// One thread per (split chain j, dim d): two-pass mean and std (ddof = 1, numpy np.std(ddof=1)).
+__global__ __launch_bounds__(256) void k_split_moments(Src s, double* mean_out, double* std_out) {
+  const int d = blockIdx.y * kDimTile + (threadIdx.x & (kDimTile - 1));
+  const int64_t j = (int64_t)blockIdx.x * (256 / kDimTile) + (threadIdx.x / kDimTile);
+  if (d >= s.D || j >= 2 * s.n_chains) return;
+  double sum = 0.0;
+  for (int t = 0; t < s.n; ++t) sum += split_ptr(s, j, t)[d];
+  const double mean = sum / s.n;
+  double m2 = 0.0;
+  for (int t = 0; t < s.n; ++t) {
+    const double e = split_ptr(s, j, t)[d] - mean;
+    m2 += e * e;
+  }
+  mean_out[j * s.D + d] = mean;
+  std_out[j * s.D + d] = sqrt(m2 / (s.n - 1));
+}
+
+struct Rows {
+  const double* x;
+  int64_t n_outer, outer_stride, n_inner, inner_stride, base;
+  int D;
+  const double* center;  // null: plain sum; else sum of (x - center_d)^2
+};
+
+// partial[chunk][d] = sum over the chunk's rows.  Block = 4 row-lanes x 64 dims.
+__global__ __launch_bounds__(256) void k_rowsum_partial(Rows r, double* partial) {
+  __shared__ double red[4][kDimTile];
+  const int dl = threadIdx.x & (kDimTile - 1);
+  const int rl = threadIdx.x / kDimTile;
+  const int d = blockIdx.y * kDimTile + dl;
+  const int64_t rows = r.n_outer * r.n_inner;
+  const int64_t r0 = (int64_t)blockIdx.x * kRowChunk;
+  double acc = 0.0;
+  if (d < r.D) {
+    const double c = r.center ? r.center[d] : 0.0;
+    for (int i = rl; i < kRowChunk; i += 4) {
+      const int64_t row = r0 + i;
+      if (row >= rows) break;
+      const int64_t o = row / r.n_inner, in = row - o * r.n_inner;
+      const double v = r.x[r.base + o * r.outer_stride + in * r.inner_stride + d];
+      if (r.center) {
+        const double e = v - c;
+        acc += e * e;
+      } else {
+        acc += v;
+      }
+    }
+  }
+  red[rl][dl] = acc;
+  __syncthreads();
+  if (rl == 0 && d < r.D)
+    partial[(int64_t)blockIdx.x * r.D + d] = ((red[0][dl] + red[1][dl]) + red[2][dl]) + red[3][dl];
+}
+
+// out[c] = sum_k partial[k][c] for c < ncols (fixed order: deterministic).
+__global__ __launch_bounds__(256) void k_colsum_final(const double* partial, int64_t nchunks, int64_t ncols,
+                                                      double* out) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncols) return;
+  double acc = 0.0;
+  for (int64_t k = 0; k < nchunks; ++k) acc += partial[k * ncols + c];
+  out[c] = acc;
+}
+
+// partial[chunk][t - t0][d] = sum over split chains j of the chunk of sum_s (x_j[s+t]-x_j[s])^2.
+__global__ __launch_bounds__(256) void k_variogram_partial(Src s, int t0, int t1, int64_t jchunk, double* partial) {
+  __shared__ double red[4][kDimTile];
+  const int dl = threadIdx.x & (kDimTile - 1);
+  const int rl = threadIdx.x / kDimTile;
+  const int d = blockIdx.y * kDimTile + dl;
+  const int64_t j0 = (int64_t)blockIdx.x * jchunk;
+  const int64_t j1 = min(j0 + jchunk, 2 * s.n_chains);
+  const int nt = t1 - t0;
+  for (int t = t0; t < t1; ++t) {
+    double acc = 0.0;
+    if (d < s.D) {
+      for (int64_t j = j0 + rl; j < j1; j += 4) {
+        const double* b = split_ptr(s, j, 0) + d;
+        for (int m = 0; m + t < s.n; ++m) {
+          const double e = b[(int64_t)(m + t) * s.sample_stride] - b[(int64_t)m * s.sample_stride];
+          acc += e * e;
+        }
+      }
+    }
+    red[rl][dl] = acc;
+    __syncthreads();
+    if (rl == 0 && d < s.D)
+      partial[((int64_t)blockIdx.x * nt + (t - t0)) * s.D + d] = ((red[0][dl] + red[1][dl]) + red[2][dl]) + red[3][dl];
+    __syncthreads();
+  }
+}
+
+int64_t rows_chunks(int64_t rows) { return (rows + kRowChunk - 1) / kRowChunk; }
+
+int64_t vario_jchunk(int64_t m2) {
+  // ~4096 blocks at most; at least 16 split chains per block
+  int64_t c = (m2 + 4095) / 4096;
+  return c < 16 ? 16 : c;
+}
+
+}  // namespace
+
+int64_t diag_rowsum_work(int64_t rows, int D) { return rows_chunks(rows) * D; }
+
+int64_t diag_variogram_work(int64_t n_chains, int D, int nlags) {
+  const int64_t m2 = 2 * n_chains;
+  const int64_t jc = vario_jchunk(m2);
+  return ((m2 + jc - 1) / jc) * (int64_t)nlags * D;
+}
+
+hipError_t launch_split_moments(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int64_t base, int n,
+                                int D, double* mean_out, double* std_out, hipStream_t st) {
+  Src s{x, cs, ss, base, n_chains, n, D};
+  const int64_t m2 = 2 * n_chains;
+  dim3 grid((unsigned)((m2 + 3) / 4), (unsigned)((D + kDimTile - 1) / kDimTile));
+  k_split_moments<<<grid, 256, 0, st>>>(s, mean_out, std_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_rowsum(const double* x, int64_t n_outer, int64_t os, int64_t n_inner, int64_t is, int64_t base,
+                         int D, const double* center, double* work, double* out, hipStream_t st) {
+  Rows r{x, n_outer, os, n_inner, is, base, D, center};
+  const int64_t nch = rows_chunks(n_outer * n_inner);
+  dim3 grid((unsigned)nch, (unsigned)((D + kDimTile - 1) / kDimTile));
+  k_rowsum_partial<<<grid, 256, 0, st>>>(r, work);
+  if (hipError_t e = hipGetLastError()) return e;
+  k_colsum_final<<<(unsigned)((D + 255) / 256), 256, 0, st>>>(work, nch, D, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_variogram(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int64_t base, int n, int D,
+                            int t0, int t1, double* work, double* out, hipStream_t st) {
+  Src s{x, cs, ss, base, n_chains, n, D};
+  const int64_t m2 = 2 * n_chains;
+  const int64_t jc = vario_jchunk(m2);
+  const int64_t nch = (m2 + jc - 1) / jc;
+  dim3 grid((unsigned)nch, (unsigned)((D + kDimTile - 1) / kDimTile));
+  k_variogram_partial<<<grid, 256, 0, st>>>(s, t0, t1, jc, work);
+  if (hipError_t e = hipGetLastError()) return e;
+  const int64_t ncols = (int64_t)(t1 - t0) * D;
+  k_colsum_final<<<(unsigned)((ncols + 255) / 256), 256, 0, st>>>(work, nch, ncols, out);
+  return hipGetLastError();
+}
+
+}  // namespace hmc

@@ -1,0 +1,114 @@
+// hmc_internal.hpp — host-side kernel argument blocks and launchers (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hmc.h"
+
+namespace hmc {
+
+// Lane-group layout of one chain inside a wave64 (see hmc_device.hpp).
+struct Layout {
+  int K;       // coordinate pairs per lane
+  int lpc;     // lanes per chain
+  int cpw;     // chains per wave
+  int npairs;  // ceil(D/2)
+};
+
+// Arguments of the diagonal-target Random-trajectory kernels (init + iterations).
+struct RandArgs {
+  int64_t n;             // chains in this call
+  int64_t chain_offset;  // global id of chain 0 (Philox key)
+  int D, npairs, lpc, cpw;
+  int niter, wu, thin, Lc, L_low, L_high, it0, it1, i_oob;
+  uint32_t k0, k1;       // Philox key (seed)
+  double dt, h, logc;    // step, dt/2, V constant
+  const double* q0;      // [D] or null
+  const double* prec;    // [D] or null
+  const double* minv;    // [D] or null
+  const double* pscale;  // [D] or null
+  const double* dtv;     // [D] or null
+  const double* rp0;     // replay streams
+  const double* rp;
+  const double* rlnu;
+  const int32_t* rL;
+  const double* qstart;  // init only
+  double* q;
+  double* Eprev;
+  double* qc;
+  double* Ec;
+  double* dEc;
+  unsigned long long* cnt;
+  double* traj_q;        // chain-0 trajectory capture (or null)
+  int32_t* traj_len;
+  int32_t* decision;
+  int n_save, traj_stride;
+};
+
+// Dense-precision (correlated MVN) Random-trajectory kernel arguments.
+struct DenseArgs {
+  int64_t n, chain_offset;
+  int D, Dp;             // D and D padded to a multiple of 16
+  int niter, wu, thin, Lc, L_low, L_high, it0, it1, i_oob;
+  uint32_t k0, k1;
+  double dt, h, logc;
+  const double* q0;      // [D] or null
+  const double* prec;    // [D*D] row-major
+  const double* minv;    // [D] or null
+  const double* pscale;  // [D] or null
+  const double* dtv;     // [D] or null
+  const double* rp0;
+  const double* rp;
+  const double* rlnu;
+  const int32_t* rL;
+  const double* qstart;
+  double* q;
+  double* Eprev;
+  double* qc;
+  double* Ec;
+  double* dEc;
+  unsigned long long* cnt;
+};
+
+Layout choose_layout(int D, int L_low, int L_high);
+
+hipError_t launch_random_init(const RandArgs& a, const Layout& lay, bool gen, bool replay, hipStream_t s);
+hipError_t launch_random_iters(const RandArgs& a, const Layout& lay, bool exact, bool gen, bool replay,
+                               hipStream_t s);
+hipError_t launch_dense_init(const DenseArgs& a, bool replay, hipStream_t s);
+hipError_t launch_dense_iters(const DenseArgs& a, bool exact, bool replay, hipStream_t s);
+
+
+// Row-wise API kernels (hmc_api_kernels.hip).
+struct RowArgs {
+  int64_t n;
+  int D;
+  int dense;
+  const double* q0;
+  const double* prec;
+  const double* minv;
+  const double* dtv;
+  double dt, logc;
+  const double* p;
+  const double* q;
+  double* po;
+  double* qo;
+  double* E;
+};
+hipError_t launch_leapfrog_rows(const RowArgs& a, bool exact, hipStream_t s);
+hipError_t launch_energy_rows(const RowArgs& a, hipStream_t s);
+hipError_t launch_philox(uint4 c, uint32_t k0, uint32_t k1, int64_t n, uint32_t* out, hipStream_t s);
+hipError_t launch_rng_normals(uint32_t k0, uint32_t k1, int64_t chain0, int64_t n, int it, int npairs,
+                              double* out, hipStream_t s);
+
+// Diagnostics (hmc_diag.hip).
+int64_t diag_rowsum_work(int64_t rows, int D);
+int64_t diag_variogram_work(int64_t n_chains, int D, int nlags);
+hipError_t launch_split_moments(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int64_t base, int n,
+                                int D, double* mean_out, double* std_out, hipStream_t st);
+hipError_t launch_rowsum(const double* x, int64_t n_outer, int64_t os, int64_t n_inner, int64_t is, int64_t base,
+                         int D, const double* center, double* work, double* out, hipStream_t st);
+hipError_t launch_variogram(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int64_t base, int n, int D,
+                            int t0, int t1, double* work, double* out, hipStream_t st);
+
+}  // namespace hmc

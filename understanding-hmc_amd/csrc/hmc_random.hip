@@ -1,0 +1,435 @@
+// hmc_random.hip — fused Random-trajectory HMC iterations for diagonal-precision MVN targets.
+//
+// Replaces the hot triple loop of HMC_sampler.gen_sample_random (samplers.py:410 -> :428 -> :448)
+// and its primitives K / E / p_sample / leap_frog (samplers.py:811-839) for targets whose
+// precision inv(cov0) is diagonal (identity in BASELINE configs 1, 2, 4).
+//
+// One launch runs iterations [it0, it1) of every chain: state q stays in registers across
+// iterations, each iteration does
+//     p ~ N(0, cov_p)                      (replay stream or in-kernel Philox + Box–Muller)
+//     E0 = V(q) + K(p)                     -> E_chain / dE_chain row            (Q14)
+//     L  ~ U{L_low..L_high-1}              (Q1)
+//     L x leap_frog with the gradient of q_new reused as the next step's q_old (bit-identical)
+//     E1, dE = E1 - E0, accept iff dE < 0 or log u < -dE
+//     store q_chain row (i - warm_up)//thin  (last write of a thinned row wins, as in Python)
+// HBM traffic per chain-iteration: one q_chain row (8D B) + E + dE (16 B); q is read/written
+// once per launch.  The arithmetic is fp64 VALU; EXACT mode keeps the reference's operation
+// order with no FMA contraction (built with -ffp-contract=off), so for diagonal targets the
+// sampled states are bit-identical to the NumPy reference on replayed streams.
+#include "hmc_device.hpp"
+#include "hmc_internal.hpp"
+
+namespace hmc {
+
+namespace {
+
+// Per-dimension constants of the general diagonal target (loaded through L1/L2; tiny).
+struct DimConst {
+  double q0, prec, minv, dt, hd;
+};
+
+template <bool GEN>
+__device__ __forceinline__ DimConst dim_const(const RandArgs& a, int d) {
+  DimConst c{0.0, 1.0, 1.0, a.dt, a.h};
+  if constexpr (GEN) {
+    if (a.q0) c.q0 = a.q0[d];
+    if (a.prec) c.prec = a.prec[d];
+    if (a.minv) c.minv = a.minv[d];
+    if (a.dtv) {
+      c.dt = a.dtv[d];
+      c.hd = c.dt * 0.5;
+    }
+  }
+  return c;
+}
+
+// Constants of coordinate slot (pair k, half h); padding slots get neutral constants and never
+// touch the per-dimension arrays.
+template <bool GEN>
+__device__ __forceinline__ DimConst slot_const(const RandArgs& a, int k, int h, bool pair_valid) {
+  const int d = 2 * k + h;
+  if (GEN && pair_valid && d < a.D) return dim_const<GEN>(a, d);
+  return DimConst{0.0, 1.0, 1.0, a.dt, a.h};
+}
+
+// Kick term (dt * (Minv * (P (q - q0)))) / 2 in the reference's operation order
+// (samplers.py:835/:837 with dVdq of case1-script.py:49).  (dt*x)/2 == (dt/2)*x exactly.
+template <bool GEN>
+__device__ __forceinline__ double kick(const DimConst& c, double q) {
+  if constexpr (GEN) {
+    return c.hd * (c.minv * (c.prec * (q - c.q0)));
+  } else {
+    return c.hd * q;
+  }
+}
+
+template <bool GEN>
+__device__ __forceinline__ void energy_terms(const DimConst& c, double q, double p, double& maha,
+                                             double& kin) {
+  if constexpr (GEN) {
+    const double x = q - c.q0;
+    maha += c.prec * x * x;
+    kin += p * (c.minv * p);
+  } else {
+    maha += q * q;
+    kin += p * p;
+  }
+}
+
+struct Lane {
+  int lane, g, s, base;
+  int64_t c;       // local chain index
+  bool active;     // lane belongs to a live chain
+  bool leader;     // first lane of a live chain's group
+};
+
+__device__ __forceinline__ Lane lane_info(const RandArgs& a) {
+  Lane L;
+  L.lane = threadIdx.x & (kWave - 1);
+  const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+  L.g = L.lane / a.lpc;
+  L.s = L.lane - L.g * a.lpc;
+  L.base = L.g * a.lpc;
+  L.c = wave * a.cpw + L.g;
+  L.active = (L.g < a.cpw) && (L.c < a.n);
+  L.leader = L.active && (L.s == 0);
+  return L;
+}
+
+template <int K, bool GEN>
+__device__ __forceinline__ double chain_energy(const RandArgs& a, const Lane& ln, const int (&kk)[K],
+                                               const bool (&pv)[K], const double (&q)[2 * K],
+                                               const double (&p)[2 * K]) {
+  double maha = 0.0, kin = 0.0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    if (pv[j]) {
+      const int d = 2 * kk[j];
+      energy_terms<GEN>(dim_const<GEN>(a, d), q[2 * j], p[2 * j], maha, kin);
+      if (d + 1 < a.D) energy_terms<GEN>(dim_const<GEN>(a, d + 1), q[2 * j + 1], p[2 * j + 1], maha, kin);
+    }
+  }
+  maha = group_sum(maha, ln.s, a.lpc, ln.base);
+  kin = group_sum(kin, ln.s, a.lpc, ln.base);
+  return 0.5 * (a.logc + maha) + kin / 2.0;  // V (utils.py:218, scipy form) + K (samplers.py:817)
+}
+
+template <int K, bool GEN, bool REPLAY>
+__device__ __forceinline__ void draw_momentum(const RandArgs& a, const Lane& ln, int it, const int (&kk)[K],
+                                              const bool (&pv)[K], double (&p)[2 * K]) {
+  const bool even = (a.D & 1) == 0;
+  const uint64_t gc = (uint64_t)(a.chain_offset + ln.c);
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    p[2 * j] = 0.0;
+    p[2 * j + 1] = 0.0;
+    if (pv[j]) {
+      const int d = 2 * kk[j];
+      if constexpr (REPLAY) {
+        const double* row = (it == 0) ? a.rp0 + ln.c * (int64_t)a.D
+                                      : a.rp + (ln.c * (int64_t)a.niter + (it - 1)) * a.D;
+        load_pair(row, kk[j], even, d + 1 < a.D, p[2 * j], p[2 * j + 1]);
+      } else {
+        normal_pair(draw_block((uint32_t)kk[j], (uint32_t)it, gc, a.k0, a.k1), p[2 * j], p[2 * j + 1]);
+        if (GEN && a.pscale) {
+          p[2 * j] *= a.pscale[d];
+          if (d + 1 < a.D) p[2 * j + 1] *= a.pscale[d + 1];
+        }
+      }
+      if (d + 1 >= a.D) p[2 * j + 1] = 0.0;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Chain initialisation (samplers.py:413-420): q_chain[:,0] = q_start, E_chain[:,0] = E(q, p0).
+template <int K, bool GEN, bool REPLAY>
+__global__ __launch_bounds__(256) void k_random_init(RandArgs a) {
+  const Lane ln = lane_info(a);
+  const bool even = (a.D & 1) == 0;
+  int kk[K];
+  bool pv[K];
+  double q[2 * K], p[2 * K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    kk[j] = ln.s + a.lpc * j;
+    pv[j] = ln.active && kk[j] < a.npairs;
+    q[2 * j] = q[2 * j + 1] = 0.0;
+    if (pv[j]) load_pair(a.qstart + ln.c * (int64_t)a.D, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);
+  }
+  draw_momentum<K, GEN, REPLAY>(a, ln, 0, kk, pv, p);
+  const double E0 = chain_energy<K, GEN>(a, ln, kk, pv, q, p);
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    if (pv[j]) {
+      const bool v1 = 2 * kk[j] + 1 < a.D;
+      store_pair(a.q + ln.c * (int64_t)a.D, kk[j], even, v1, q[2 * j], q[2 * j + 1]);
+      if (a.qc) store_pair(a.qc + ln.c * (int64_t)a.Lc * a.D, kk[j], even, v1, q[2 * j], q[2 * j + 1]);
+    }
+  }
+  if (ln.leader) {
+    a.Eprev[ln.c] = E0;
+    if (a.Ec) a.Ec[ln.c * (int64_t)a.Lc] = E0;
+    if (a.dEc) a.dEc[ln.c * (int64_t)a.Lc] = 0.0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Iterations [it0, it1) (samplers.py:428-475).
+template <int K, bool EXACT, bool GEN, bool REPLAY>
+__global__ __launch_bounds__(256) void k_random_iters(RandArgs a) {
+  const Lane ln = lane_info(a);
+  const bool even = (a.D & 1) == 0;
+  const uint64_t gc = (uint64_t)(a.chain_offset + ln.c);
+  int kk[K];
+  bool pv[K];
+  double q[2 * K], p[2 * K], qi[2 * K], t[2 * K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    kk[j] = ln.s + a.lpc * j;
+    pv[j] = ln.active && kk[j] < a.npairs;
+    q[2 * j] = q[2 * j + 1] = 0.0;
+    if (pv[j]) load_pair(a.q + ln.c * (int64_t)a.D, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);
+  }
+  double Eprev = ln.active ? a.Eprev[ln.c] : 0.0;
+  unsigned long long n_acc = 0, n_acc_wu = 0, n_lf = 0, n_lf2 = 0, n_oob = 0;
+
+  for (int it = a.it0; it < a.it1; ++it) {
+    // ---- momentum resample (samplers.py:431) and initial energy (:434)
+    draw_momentum<K, GEN, REPLAY>(a, ln, it, kk, pv, p);
+    const double E0 = chain_energy<K, GEN>(a, ln, kk, pv, q, p);
+    const bool post = it >= a.wu;
+    const bool write_row = post && ((it == a.niter) || ((it - a.wu + 1) % a.thin == 0));
+    const int64_t row = post ? (int64_t)((it - a.wu) / a.thin) : 0;
+    if (ln.leader && write_row) {                       // :436-438 (Q14)
+      if (a.Ec) a.Ec[ln.c * (int64_t)a.Lc + row] = E0;
+      if (a.dEc) a.dEc[ln.c * (int64_t)a.Lc + row] = E0 - Eprev;
+    }
+    Eprev = E0;                                          // :460
+
+    // ---- trajectory length (:441) and log-uniform for the MH test (:461)
+    int L;
+    double lnu;
+    if constexpr (REPLAY) {
+      L = ln.active ? a.rL[ln.c * (int64_t)a.niter + (it - 1)] : 0;
+      lnu = ln.active ? a.rlnu[ln.c * (int64_t)a.niter + (it - 1)] : 0.0;
+    } else {
+      const uint4 r = draw_block(kDrawSlot, (uint32_t)it, gc, a.k0, a.k1);
+      L = ln.active ? uniform_int(r.x, a.L_low, a.L_high) : 0;
+      lnu = log(u53(r.z, r.w));
+    }
+
+    // ---- chain-0 trajectory capture (samplers.py:442-452): lane holding dims 0,1 records q[:2]
+    const bool cap = a.traj_q && (gc == 0) && (it <= a.n_save) && ln.leader;
+    double* capp = cap ? a.traj_q + (int64_t)(it - 1) * a.traj_stride * 2 : nullptr;
+    if (cap) {
+      capp[0] = q[0];
+      capp[1] = a.D > 1 ? q[1] : q[0];
+    }
+
+    // ---- L leapfrog steps (:448-450 -> :831-839)
+#pragma unroll
+    for (int e = 0; e < 2 * K; ++e) qi[e] = q[e];
+    if constexpr (EXACT) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) t[2 * j + h] = kick<GEN>(slot_const<GEN>(a, kk[j], h, pv[j]), q[2 * j + h]);
+      }
+      for (int l = 0; l < L; ++l) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int e = 2 * j + h;
+            const DimConst c = slot_const<GEN>(a, kk[j], h, pv[j]);
+            const double ph = p[e] - t[e];              // p_half = p_old - dt*(M^-1 dVdq(q_old))/2
+            q[e] = q[e] + c.dt * ph;                    // q_new  = q_old + dt*p_half
+            t[e] = kick<GEN>(c, q[e]);                  // dt*(M^-1 dVdq(q_new))/2, reused next step
+            p[e] = ph - t[e];                           // p_new  = p_half - ...
+          }
+        }
+        if (cap) {
+          capp[2 * (l + 1)] = q[0];
+          capp[2 * (l + 1) + 1] = a.D > 1 ? q[1] : q[0];
+        }
+      }
+    } else {
+      for (int l = 0; l < L; ++l) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int e = 2 * j + h;
+            const DimConst c = slot_const<GEN>(a, kk[j], h, pv[j]);
+            const double cc = GEN ? c.hd * (c.minv * c.prec) : c.hd;
+            const double ph = __builtin_fma(-cc, q[e] - c.q0, p[e]);
+            q[e] = __builtin_fma(c.dt, ph, q[e]);
+            p[e] = __builtin_fma(-cc, q[e] - c.q0, ph);
+          }
+        }
+        if (cap) {
+          capp[2 * (l + 1)] = q[0];
+          capp[2 * (l + 1) + 1] = a.D > 1 ? q[1] : q[0];
+        }
+      }
+    }
+    // lanes whose slot is past D carry zeros; keep them zero
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (!pv[j] || 2 * kk[j] + 1 >= a.D) {
+        q[2 * j + 1] = 0.0;
+        p[2 * j + 1] = 0.0;
+        if (!pv[j]) q[2 * j] = p[2 * j] = 0.0;
+      }
+    }
+
+    // ---- final energy and Metropolis test (:455-472)
+    const double E1 = chain_energy<K, GEN>(a, ln, kk, pv, q, p);
+    const double dE = E1 - E0;
+    const bool accept = (dE < 0.0) || (lnu < -dE);
+    if (!accept) {
+#pragma unroll
+      for (int e = 0; e < 2 * K; ++e) q[e] = qi[e];
+    }
+    if (write_row && a.qc) {
+      double* rowp = a.qc + (ln.c * (int64_t)a.Lc + row) * a.D;
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        if (pv[j]) store_pair(rowp, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);
+    }
+    if (cap) {
+      a.traj_len[it - 1] = (L > 0 ? L : 0) + 1;
+      a.decision[it - 1] = accept ? 1 : 0;
+    }
+    if (ln.leader) {
+      if (accept) {
+        if (post) ++n_acc; else ++n_acc_wu;
+      } else if (it < a.i_oob) {
+        ++n_oob;                                         // reference would raise IndexError (Q5)
+      }
+      const unsigned long long Lp = L > 0 ? (unsigned long long)L : 0ull;  // xrange(1, L+1) is empty for L <= 0
+      n_lf += Lp;
+      n_lf2 += Lp * Lp;
+    }
+  }
+
+  // ---- state write-back and counters
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+    if (pv[j]) store_pair(a.q + ln.c * (int64_t)a.D, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);
+  if (ln.leader) a.Eprev[ln.c] = Eprev;
+  n_acc = wave_sum_u64(n_acc);
+  n_acc_wu = wave_sum_u64(n_acc_wu);
+  n_lf = wave_sum_u64(n_lf);
+  n_lf2 = wave_sum_u64(n_lf2);
+  n_oob = wave_sum_u64(n_oob);
+  if (ln.lane == 0 && a.cnt) {
+    if (n_acc) atomicAdd(a.cnt + HMC_CNT_ACCEPT, n_acc);
+    if (n_acc_wu) atomicAdd(a.cnt + HMC_CNT_ACCEPT_WU, n_acc_wu);
+    if (n_lf) atomicAdd(a.cnt + HMC_CNT_LEAPFROG, n_lf);
+    if (n_lf2) atomicAdd(a.cnt + HMC_CNT_LEAPFROG_SQ, n_lf2);
+    if (n_oob) atomicAdd(a.cnt + HMC_CNT_OOB_REJECT, n_oob);
+  }
+}
+
+template <int K>
+hipError_t launch_init_k(const RandArgs& a, bool gen, bool replay, dim3 grid, hipStream_t s) {
+  if (gen) {
+    if (replay) k_random_init<K, true, true><<<grid, 256, 0, s>>>(a);
+    else k_random_init<K, true, false><<<grid, 256, 0, s>>>(a);
+  } else {
+    if (replay) k_random_init<K, false, true><<<grid, 256, 0, s>>>(a);
+    else k_random_init<K, false, false><<<grid, 256, 0, s>>>(a);
+  }
+  return hipGetLastError();
+}
+
+template <int K, bool EXACT>
+hipError_t launch_iters_k2(const RandArgs& a, bool gen, bool replay, dim3 grid, hipStream_t s) {
+  if (gen) {
+    if (replay) k_random_iters<K, EXACT, true, true><<<grid, 256, 0, s>>>(a);
+    else k_random_iters<K, EXACT, true, false><<<grid, 256, 0, s>>>(a);
+  } else {
+    if (replay) k_random_iters<K, EXACT, false, true><<<grid, 256, 0, s>>>(a);
+    else k_random_iters<K, EXACT, false, false><<<grid, 256, 0, s>>>(a);
+  }
+  return hipGetLastError();
+}
+
+template <int K>
+hipError_t launch_iters_k(const RandArgs& a, bool exact, bool gen, bool replay, dim3 grid, hipStream_t s) {
+  return exact ? launch_iters_k2<K, true>(a, gen, replay, grid, s)
+               : launch_iters_k2<K, false>(a, gen, replay, grid, s);
+}
+
+dim3 grid_for(const RandArgs& a) {
+  const int64_t waves = (a.n + a.cpw - 1) / a.cpw;
+  return dim3((unsigned)((waves + 3) / 4));
+}
+
+}  // namespace
+
+// E[max of c iid U{lo..hi-1}] — the wave runs as long as its longest trajectory.
+static double expected_max(int lo, int hi, int c) {
+  const int n = hi - lo;
+  if (n <= 1 || c <= 1) return 0.5 * (lo + hi - 1);
+  double e = 0.0, prev = 0.0;
+  for (int x = lo; x < hi; ++x) {
+    const double F = pow((double)(x - lo + 1) / n, c);
+    e += x * (F - prev);
+    prev = F;
+  }
+  return e;
+}
+
+Layout choose_layout(int D, int L_low, int L_high) {
+  static const int Ks[] = {1, 2, 4, 5, 8, 16};
+  Layout best{0, 0, 0, (D + 1) / 2};
+  double best_score = -1.0;
+  const double mean = 0.5 * (L_low + L_high - 1);
+  for (int K : Ks) {
+    const int lpc = (best.npairs + K - 1) / K;
+    if (lpc > kWave) continue;
+    const int cpw = kWave / lpc;
+    const double util = (double)best.npairs * cpw / (kWave * (double)K);
+    const double emax = expected_max(L_low, L_high, cpw);
+    const double score = util * (emax > 0 ? mean / emax : 1.0);
+    if (score > best_score + 1e-9) {
+      best_score = score;
+      best.K = K;
+      best.lpc = lpc;
+      best.cpw = cpw;
+    }
+  }
+  return best;
+}
+
+hipError_t launch_random_init(const RandArgs& a, const Layout& lay, bool gen, bool replay, hipStream_t s) {
+  const dim3 grid = grid_for(a);
+  switch (lay.K) {
+    case 1: return launch_init_k<1>(a, gen, replay, grid, s);
+    case 2: return launch_init_k<2>(a, gen, replay, grid, s);
+    case 4: return launch_init_k<4>(a, gen, replay, grid, s);
+    case 5: return launch_init_k<5>(a, gen, replay, grid, s);
+    case 8: return launch_init_k<8>(a, gen, replay, grid, s);
+    case 16: return launch_init_k<16>(a, gen, replay, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_random_iters(const RandArgs& a, const Layout& lay, bool exact, bool gen, bool replay,
+                               hipStream_t s) {
+  const dim3 grid = grid_for(a);
+  switch (lay.K) {
+    case 1: return launch_iters_k<1>(a, exact, gen, replay, grid, s);
+    case 2: return launch_iters_k<2>(a, exact, gen, replay, grid, s);
+    case 4: return launch_iters_k<4>(a, exact, gen, replay, grid, s);
+    case 5: return launch_iters_k<5>(a, exact, gen, replay, grid, s);
+    case 8: return launch_iters_k<8>(a, exact, gen, replay, grid, s);
+    case 16: return launch_iters_k<16>(a, exact, gen, replay, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace hmc

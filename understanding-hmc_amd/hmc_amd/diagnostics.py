@@ -1,0 +1,205 @@
+"""Split-chain R-hat / ESS and per-dimension mean/std, computed on the GPU.
+
+Same estimators as the reference (utils.py:77-179; samplers.py:213, :246),
+including its quirks: W is the mean of per-split-chain *standard deviations*
+(Q8) and the ESS early exit tests rho_1 twice (Q9).  Heavy sums run in the
+libhmc.so diagnostics kernels; the O(D) combination and the ESS termination
+loop (which only touches per-lag, per-dimension scalars) run on the host.
+
+Multi-GPU: every sum is additive over chains, so with `group` (a
+torch.distributed process group; RCCL over xGMI on MI355X) each rank reduces
+its own chains and `all_reduce` combines the per-dimension sums.
+"""
+import numpy as np
+import torch
+
+from . import _lib as H
+
+_LAG_BLOCK = 32
+
+
+def _as_device(x):
+    """(Nchain, T, D) float64 CUDA tensor view (no copy when already on the device)."""
+    if isinstance(x, torch.Tensor):
+        t = x if x.dtype == torch.float64 else x.double()
+        if not t.is_cuda:
+            t = t.cuda()
+    else:
+        t = torch.as_tensor(np.asarray(x, dtype=np.float64)).cuda()
+    if t.stride(2) != 1:
+        t = t.contiguous()
+    return t
+
+
+def _stream(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _allreduce(x, group):
+    if group is not None:
+        torch.distributed.all_reduce(x, group=group)
+    return x
+
+
+class _Split:
+    """Strided view of the split chains of convergence_stats (utils.py:88-104)."""
+
+    def __init__(self, q_chain, thin_rate, warm_up_num):
+        t = _as_device(q_chain)
+        self.t = t
+        Nchain, Niter, D = t.shape
+        self.Nchain, self.D = Nchain, D
+        Lt = len(range(warm_up_num, Niter, thin_rate))       # rows of q_chain[m, wu:][::thin]
+        self.n = Lt // 2                                       # utils.py:102 (Py2 int division)
+        self.ptr = t.data_ptr()                                # points at element [0, 0, 0] of the view
+        self.base = warm_up_num * t.stride(1)
+        self.cs = t.stride(0)
+        self.ss = t.stride(1) * thin_rate
+
+
+def split_moments(sp):
+    L = H.lib()
+    m2 = 2 * sp.Nchain
+    mean = torch.empty((m2, sp.D), dtype=torch.float64, device=sp.t.device)
+    std = torch.empty_like(mean)
+    H.check(L.hmc_split_moments(sp.ptr, sp.Nchain, sp.cs, sp.ss, sp.base, sp.n, sp.D, H.ptr(mean), H.ptr(std),
+                                _stream(sp.t)), "hmc_split_moments")
+    return mean, std
+
+
+def _rowsum(x2d, center=None):
+    """Column sums of a contiguous (rows, D) device matrix (or of (x - center)^2)."""
+    L = H.lib()
+    rows, D = x2d.shape
+    work = torch.empty(max(1, L.hmc_rowsum_work_size(rows, D)), dtype=torch.float64, device=x2d.device)
+    out = torch.empty(D, dtype=torch.float64, device=x2d.device)
+    H.check(L.hmc_rowsum(H.ptr(x2d), rows, D, 1, 0, 0, D, H.ptr(center), H.ptr(work), H.ptr(out),
+                         _stream(x2d)), "hmc_rowsum")
+    return out
+
+
+def variogram_sums(sp, t0, t1):
+    """sum_j sum_s (x_j[s+t]-x_j[s])^2 for t in [t0, t1) -> (t1-t0, D) device tensor."""
+    L = H.lib()
+    work = torch.empty(max(1, L.hmc_variogram_work_size(sp.Nchain, sp.D, t1 - t0)), dtype=torch.float64,
+                       device=sp.t.device)
+    out = torch.empty((t1 - t0, sp.D), dtype=torch.float64, device=sp.t.device)
+    H.check(L.hmc_variogram(sp.ptr, sp.Nchain, sp.cs, sp.ss, sp.base, sp.n, sp.D, t0, t1, H.ptr(work), H.ptr(out),
+                            _stream(sp.t)), "hmc_variogram")
+    return out
+
+
+def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
+    """utils.py:77-159 on the GPU.  q_chain: (Nchain, Niter, D) NumPy array or CUDA tensor
+    (views such as q_chain_device[:, 1:, :] are read in place).  Returns (R, n_eff) NumPy."""
+    sp = _Split(q_chain, thin_rate, warm_up_num)
+    n_local = torch.tensor([float(sp.Nchain)], dtype=torch.float64, device=sp.t.device)
+    Nchain = int(_allreduce(n_local, group).item())
+    assert Nchain > 1                                                   # utils.py:85
+    n, D = sp.n, sp.D
+    m = 2 * Nchain
+    mean, std = split_moments(sp)
+    s1 = torch.stack([_rowsum(std), _rowsum(mean)])                    # sum_j std_j, sum_j mean_j
+    _allreduce(s1, group)
+    W = s1[0] / m                                                       # utils.py:112 (Q8)
+    mean_all = s1[1] / m                                                # :119
+    bsum = _allreduce(_rowsum(mean, center=mean_all), group)
+    B = bsum * n / float(m - 1)                                         # :120
+    var = W * (n - 1) / float(n) + B / float(n)                         # :123
+    R = torch.sqrt(var / W)                                             # :126
+    var_h = var.cpu().numpy()
+    # ---- ESS (utils.py:128-157): lags fetched in blocks until every dim has terminated
+    Vt = np.zeros((0, D))
+    need = np.ones(D, dtype=bool)
+    n_eff = np.zeros(D)
+    tmax = max(n - 1, 2)
+    t_done = 0
+    while True:
+        # lags required so far: 1, 2 always; more while any dim is still running
+        t1 = min(t_done + _LAG_BLOCK, tmax) + 1
+        if t1 > t_done + 1:
+            v = _allreduce(variogram_sums(sp, t_done + 1, t1), group).cpu().numpy()
+            lags = np.arange(t_done + 1, t1)
+            v = v / (m * (n - lags))[:, None]                           # utils.py:177
+            Vt = np.vstack([Vt, v])
+            t_done = t1 - 1
+        still = False
+        for i in np.nonzero(need)[0]:
+            res = _ess_dim(Vt[:, i], var_h[i], n, m, t_done >= tmax)
+            if res is None:
+                still = True
+            else:
+                n_eff[i] = res
+                need[i] = False
+        if not still:
+            break
+    return R.cpu().numpy(), n_eff
+
+
+def _ess_dim(Vt, var, n, m, complete):
+    """The termination loop of utils.py:130-157 given V_1..V_T (Vt[t-1]); None if more lags
+    are needed (and not all lags are available yet)."""
+    def V(t):
+        return Vt[t - 1] if t - 1 < len(Vt) else None
+    v1, v2 = V(1), V(2)
+    if v1 is None or (v2 is None and not complete):
+        return None
+    with np.errstate(all="ignore"):
+        rho1 = 1. - v1 / (2 * var)
+        rho2 = 1. - v2 / (2 * var) if v2 is not None else np.nan
+    if (rho1 < 1e-2) or (rho1 < 1e-2):                                  # Q9 (sic)
+        sum_rho = 0
+    else:
+        rho = [rho1, rho2]
+        t = 1
+        while t < n - 2:
+            vt = V(t + 2)
+            if vt is None:
+                return None
+            rho.append(1 - vt / (2 * var))
+            if ((t % 2) == 1) & ((rho[t] + rho[t + 1]) < 0):
+                break
+            t += 1
+        sum_rho = np.sum(rho[:t])
+        if sum_rho < 0:
+            sum_rho = 0
+    return m * n / (1 + 2 * sum_rho)
+
+
+def variogram(chains, var_num, t_lag):
+    """utils.py:161-179 for a list of (n, D) split chains (host arrays; API parity)."""
+    m = len(chains)
+    n = chains[0].shape[0]
+    st = torch.as_tensor(np.stack([np.asarray(c, dtype=np.float64) for c in chains])).cuda()
+    # treat each given chain as one "half": pair them as (2k, 2k+1) views of a (m/2, 2n, D) layout
+    q = st.reshape(m, n, -1)
+    sp = _Split.__new__(_Split)
+    sp.t, sp.Nchain, sp.D, sp.n = q, (m + 1) // 2, q.shape[2], n
+    sp.ptr, sp.base, sp.cs, sp.ss = q.data_ptr(), 0, 2 * n * q.shape[2], q.shape[2]
+    if m % 2:
+        raise AssertionError("variogram on an odd number of split chains is not supported on the GPU path")
+    v = variogram_sums(sp, t_lag, t_lag + 1).cpu().numpy()[0, var_num]
+    return v / float(m * (n - t_lag))
+
+
+def per_dim_mean_std(q_chain, group=None):
+    """np.mean / np.std over q_chain[:, 1:, i] per dimension (samplers.py:213, :246; Q16)."""
+    t = _as_device(q_chain)
+    N, T, D = t.shape
+    L = H.lib()
+    rows = N * (T - 1)
+    work = torch.empty(max(1, L.hmc_rowsum_work_size(rows, D)), dtype=torch.float64, device=t.device)
+    s = torch.empty(D, dtype=torch.float64, device=t.device)
+    base = t.stride(1)
+    H.check(L.hmc_rowsum(t.data_ptr(), N, t.stride(0), T - 1, t.stride(1), base, D, None, H.ptr(work), H.ptr(s),
+                         _stream(t)), "hmc_rowsum")
+    cnt = torch.tensor([float(rows)], dtype=torch.float64, device=t.device)
+    _allreduce(s, group)
+    _allreduce(cnt, group)
+    mean = s / cnt
+    m2 = torch.empty(D, dtype=torch.float64, device=t.device)
+    H.check(L.hmc_rowsum(t.data_ptr(), N, t.stride(0), T - 1, t.stride(1), base, D, H.ptr(mean), H.ptr(work),
+                         H.ptr(m2), _stream(t)), "hmc_rowsum")
+    _allreduce(m2, group)
+    std = torch.sqrt(m2 / cnt)
+    return mean.cpu().numpy(), std.cpu().numpy()

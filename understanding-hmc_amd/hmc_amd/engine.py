@@ -1,0 +1,106 @@
+"""Device-resident chain batch: buffers + C-ABI calls for the Random-trajectory sampler.
+
+`RandomEngine` owns the (Nchain x D) state and the output arrays as torch CUDA
+tensors (memory/streams only — all arithmetic is in libhmc.so) and exposes the
+two calls of the hot path: `init()` (samplers.py:413-420) and `run(it0, it1)`
+(iterations of samplers.py:428-475, fused in one kernel launch).  HMC_sampler
+and bench.py are both thin layers over it.
+"""
+import numpy as np
+import torch
+
+from . import _lib as H
+
+
+def _dev(a, device, dtype=torch.float64):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).to(device)
+
+
+class RandomEngine:
+    def __init__(self, target, n_chains, n_iter, warm_up, thin, L_low, L_high, dt, cov_p=None, rng="philox",
+                 seed=0, fp_mode="fast", chain_offset=0, store_chain=True, store_energy=True, n_save=0,
+                 device=None):
+        self.t = target
+        self.D = D = target.D
+        self.N = int(n_chains)
+        self.n_iter, self.warm_up, self.thin = int(n_iter), int(warm_up), int(thin)
+        self.L_chain = 1 + (self.n_iter - self.warm_up) // self.thin
+        self.L_low, self.L_high = int(L_low), int(L_high)
+        self.rng, self.seed, self.fp_mode = rng, int(seed), fp_mode
+        self.chain_offset = int(chain_offset)
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        dev = self.device
+        # ---- target / kinetic descriptors (kept alive on the object)
+        kind = H.HMC_TARGET_DIAG if target.diagonal else H.HMC_TARGET_DENSE
+        self._q0 = None if target.zero_mean else _dev(target.q0, dev)
+        if target.diagonal:
+            self._prec = None if target.identity else _dev(np.diag(target.prec), dev)
+        else:
+            self._prec = _dev(target.prec, dev)
+        cov_p = np.diag(np.ones(D)) if cov_p is None else np.asarray(cov_p, dtype=np.float64)
+        if np.any(cov_p - np.diag(np.diag(cov_p))):
+            raise NotImplementedError("non-diagonal cov_p: the GPU kernels support a diagonal mass matrix")
+        self.cov_p = cov_p
+        minv = np.diag(np.linalg.inv(cov_p)).astype(np.float64)      # samplers.py:356
+        ident_mass = bool(np.all(np.diag(cov_p) == 1.0) and np.all(minv == 1.0))
+        self._minv = None if ident_mass else _dev(minv, dev)
+        self._pscale = None if ident_mass else _dev(np.sqrt(np.diag(cov_p)), dev)
+        dt = np.asarray(dt, dtype=np.float64)
+        if dt.ndim == 0:
+            self._dtv, dts = None, float(dt)
+        else:
+            assert dt.size == D
+            self._dtv, dts = _dev(dt.reshape(-1), dev), 0.0
+        self.T = H.Target(D, kind, H.ptr(self._q0), H.ptr(self._prec), target.logdet_const)
+        self.K = H.Kinetic(H.ptr(self._minv), H.ptr(self._pscale), H.ptr(self._dtv), dts)
+        # ---- state and outputs
+        N, Lc = self.N, self.L_chain
+        self.q = torch.zeros((N, D), dtype=torch.float64, device=dev)
+        self.E_prev = torch.zeros(N, dtype=torch.float64, device=dev)
+        self.q_chain = torch.zeros((N, Lc, D), dtype=torch.float64, device=dev) if store_chain else None
+        self.E_chain = torch.zeros((N, Lc), dtype=torch.float64, device=dev) if store_energy else None
+        self.dE_chain = torch.zeros((N, Lc), dtype=torch.float64, device=dev) if store_energy else None
+        self.counters = torch.zeros(H.NCOUNTERS, dtype=torch.int64, device=dev)
+        self.n_save = int(n_save)
+        if self.n_save:
+            self.traj_stride = max(self.L_high, 1)
+            self.traj = torch.zeros((self.n_save, self.traj_stride, 2), dtype=torch.float64, device=dev)
+            self.traj_len = torch.zeros(self.n_save, dtype=torch.int32, device=dev)
+            self.decision = torch.zeros(self.n_save, dtype=torch.int32, device=dev)
+        else:
+            self.traj_stride, self.traj, self.traj_len, self.decision = 0, None, None, None
+        self.S = H.State(H.ptr(self.q), H.ptr(self.E_prev), H.ptr(self.q_chain), H.ptr(self.E_chain),
+                         H.ptr(self.dE_chain), H.ptr(self.counters), H.ptr(self.traj), H.ptr(self.traj_len),
+                         H.ptr(self.decision), self.n_save, self.traj_stride)
+        self._replay = None
+        self._streams = []
+
+    def set_replay(self, p0, P, Ls, lnu):
+        """Host-replayed draws (rng='replay'): p0 (N,D), p (N,Niter,D), L (N,Niter), log u (N,Niter)."""
+        dev = self.device
+        self._streams = [_dev(p0, dev), _dev(P, dev), _dev(Ls, dev, torch.int32), _dev(lnu, dev)]
+        self._replay = H.Replay(*[H.ptr(x) for x in self._streams], None, 0)
+
+    def schedule(self, it0, it1):
+        return H.Schedule(self.N, self.chain_offset, self.n_iter, self.warm_up, self.thin, self.L_chain,
+                          self.L_low, self.L_high, it0, it1,
+                          H.HMC_RNG_REPLAY if self.rng == "replay" else H.HMC_RNG_PHILOX,
+                          H.HMC_MODE_EXACT if self.fp_mode == "exact" else H.HMC_MODE_FAST, 10, 0, self.seed)
+
+    def stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def init(self, q_start):
+        qs = q_start if isinstance(q_start, torch.Tensor) else _dev(np.asarray(q_start).reshape(self.N, self.D),
+                                                                    self.device)
+        self._qs = qs.to(self.device, torch.float64).contiguous()
+        H.check(H.lib().hmc_chain_init(self.T, self.K, self.schedule(1, 1), self._replay, H.ptr(self._qs), self.S,
+                                       self.stream()), "hmc_chain_init")
+
+    def run(self, it0, it1):
+        """Iterations [it0, it1) of every chain in ONE fused kernel launch."""
+        H.check(H.lib().hmc_random_iters(self.T, self.K, self.schedule(it0, it1), self._replay, self.S,
+                                         self.stream()), "hmc_random_iters")
+
+    def read_counters(self):
+        return self.counters.cpu().numpy().astype(np.int64)

@@ -1,0 +1,50 @@
+"""Helpers with the reference `utils.py` names (utils.py:77-218).
+
+`start_pts` and `normal_lnL` are the host helpers the drivers call to build
+their inputs (they stay NumPy/SciPy, as in the reference).  `convergence_stats`
+(split-chain R-hat and ESS, utils.py:77-159) runs on the GPU through the
+diagnostics kernels of libhmc.so (diagnostics.py); NUTS bookkeeping helpers are
+restated as integer bit logic (the GPU NUTS kernel uses the same closed forms).
+"""
+import numpy as np
+from scipy.stats import multivariate_normal
+
+from .diagnostics import convergence_stats, per_dim_mean_std, variogram  # noqa: F401
+
+
+def start_pts(q0, cov0, size):
+    """utils.py:204-209 (host draw from the global legacy RNG, exactly as the reference)."""
+    return np.random.multivariate_normal(q0, cov0, size=size)
+
+
+def normal_lnL(q, q0, cov0):
+    """utils.py:213-218."""
+    return multivariate_normal.logpdf(q, mean=q0, cov=cov0)
+
+
+def check_points(m):
+    """utils.py:246-283 in closed form: for even m, the first point of every aligned
+    power-of-two sub-tree (size >= 2) ending at m."""
+    assert (m % 2) == 0
+    r = int(m)
+    while (r & (r - 1)) != 0 and r > 2:
+        r -= 1 << (r.bit_length() - 1)
+    pts = [m - r + 1]
+    half = r
+    while half > 2:
+        half >>= 1
+        pts.append(pts[-1] + half)
+    return np.asarray(pts)
+
+
+def release_fast(m, l):
+    """utils.py:367-385."""
+    r_m, r_l = int(m), int(l)
+    while (r_m & (r_m - 1)) != 0 and r_m > 4:
+        top = 1 << (r_m.bit_length() - 1)
+        r_m -= top
+        r_l -= top
+    return (r_m >= 4) and (r_l > 1)
+
+
+release = release_fast   # utils.py:286-304 implements the same rule (with an assert)
