@@ -208,3 +208,42 @@ def test_fp_modes_agree_statistically():
     hf, _ = _philox_run(N, D, 10, 2, fp_mode="fast")
     # same draws, trajectories differ only by FMA rounding: tiny differences everywhere
     np.testing.assert_allclose(he.q_chain, hf.q_chain, rtol=1e-8, atol=1e-8)
+
+
+def _np_philox(ctr, key):
+    """Vectorised NumPy Philox4x32-10 (ctr: (n,4) uint64 words, key: (2,) ints)."""
+    c = [ctr[:, i].astype(np.uint64) for i in range(4)]
+    k0, k1 = np.uint64(key[0]), np.uint64(key[1])
+    M = np.uint64(0xFFFFFFFF)
+    for _ in range(10):
+        p0 = c[0] * np.uint64(0xD2511F53)
+        p1 = c[2] * np.uint64(0xCD9E8D57)
+        c = [((p1 >> np.uint64(32)) ^ c[1] ^ k0) & M, p1 & M, ((p0 >> np.uint64(32)) ^ c[3] ^ k1) & M, p0 & M]
+        k0 = (k0 + np.uint64(0x9E3779B9)) & M
+        k1 = (k1 + np.uint64(0xBB67AE85)) & M
+    return c
+
+
+def test_philox_normals_match_numpy_box_muller():
+    """The in-kernel fp64 Box-Muller (custom ~1-ulp log/sqrt/sincospi) agrees with NumPy's
+    libm-based Box-Muller on the same Philox words to a few ulp (absolute, scaled by the radius)."""
+    from hmc_amd import _lib as H
+    L = H.lib()
+    n, npairs, it, seed = 4096, 16, 5, 0x1234_5678_9abc
+    out = torch.empty((n, 2 * npairs), dtype=torch.float64, device="cuda")
+    H.check(L.hmc_rng_normals(seed, 77, n, it, npairs, out.data_ptr(), None))
+    got = out.cpu().numpy().reshape(n, npairs, 2)
+    rows = np.repeat(np.arange(n, dtype=np.uint64) + np.uint64(77), npairs)
+    ks = np.tile(np.arange(npairs, dtype=np.uint64), n)
+    ctr = np.stack([ks, np.full_like(ks, it), rows & np.uint64(0xFFFFFFFF), rows >> np.uint64(32)], axis=1)
+    w = _np_philox(ctr, (seed & 0xFFFFFFFF, seed >> 32))
+    a = ((w[1] << np.uint64(21)) | (w[0] >> np.uint64(11))).astype(np.float64)
+    b = ((w[3] << np.uint64(21)) | (w[2] >> np.uint64(11))).astype(np.float64)
+    u1 = (a + 1.0) * 2.0 ** -53
+    u2 = b * 2.0 ** -53
+    r = np.sqrt(-2.0 * np.log(u1))
+    z0 = r * np.cos(2 * np.pi * u2)
+    z1 = r * np.sin(2 * np.pi * u2)
+    ref = np.stack([z0, z1], axis=1).reshape(n, npairs, 2)
+    err = np.abs(got - ref) / (r.reshape(n, npairs, 1) + 1e-300)
+    assert err.max() < 2e-15, err.max()

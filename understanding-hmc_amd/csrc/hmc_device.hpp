@@ -22,9 +22,10 @@ constexpr uint32_t kDrawSlot = 0x80000000u;  // counter.x for non-momentum draws
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
-    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    // one v_mad_u64_u32 per 32x32->64 product (lo and hi words together)
+    const uint64_t p0 = (uint64_t)c.x * 0xD2511F53u;
+    const uint64_t p1 = (uint64_t)c.z * 0xCD9E8D57u;
+    c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0);
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
@@ -45,13 +46,84 @@ __device__ __forceinline__ double u53_open0(uint32_t lo, uint32_t hi) {
   return ((double)((((uint64_t)hi) << 21) | (lo >> 11)) + 1.0) * 0x1p-53;
 }
 
+// ---- fp64 elementary functions for Box–Muller: ~1 ulp, straight-line (no double-double
+// intermediate like the libm/ocml versions, which cost ~3x more).  Algorithms: fdlibm
+// e_log.c (Lg1..Lg7 minimax on s = f/(2+f)) and k_sin.c / k_cos.c (|a| <= pi/4).
+
+// 1/d: v_rcp_f64 seed + two Newton steps.
+__device__ __forceinline__ double rcp_nr(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+
+// log(x) for finite x > 0.
+__device__ __forceinline__ double fast_log(double x) {
+  int k = __builtin_amdgcn_frexp_exp(x);
+  double m = __builtin_amdgcn_frexp_mant(x);       // [0.5, 1)
+  if (m < 0.70710678118654752440) {                 // -> [sqrt(1/2), sqrt(2))
+    m *= 2.0;
+    k -= 1;
+  }
+  const double f = m - 1.0;
+  const double hfsq = 0.5 * f * f;
+  const double s = f * rcp_nr(2.0 + f);
+  const double z = s * s, w = z * z;
+  const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 + w * 1.531383769920937332e-01));
+  const double t2 = z * (6.666666666666735130e-01 +
+                         w * (2.857142874366239149e-01 + w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
+  const double R = t2 + t1;
+  const double dk = (double)k;
+  return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
+}
+
+// sqrt(x) for x >= 0: v_rsq_f64 seed + one Goldschmidt/Newton refinement.
+__device__ __forceinline__ double fast_sqrt(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = __builtin_fma(-g, h, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  const double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  return x > 0.0 ? g : 0.0;
+}
+
+// sin(pi x), cos(pi x) for x in [0, 2].
+__device__ __forceinline__ void fast_sincospi(double x, double& sn, double& cs) {
+  const double n = __builtin_rint(2.0 * x);
+  const double r = __builtin_fma(-0.5, n, x);                    // exact, |r| <= 1/4
+  const double a = __builtin_fma(r, 3.14159265358979311600e+00, r * 1.22464679914735317720e-16);
+  const double z = a * a;
+  const double v = z * a;
+  const double sr = 8.33333333332248946124e-03 +
+                    z * (-1.98412698298579493134e-04 +
+                         z * (2.75573137070700676789e-06 + z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)));
+  const double sa = a + v * (-1.66666666666666324348e-01 + z * sr);
+  const double cr = z * (4.16666666666666019037e-02 +
+                         z * (-1.38888888888741095749e-03 +
+                              z * (2.48015872894767294178e-05 +
+                                   z * (-2.75573143513906633035e-07 +
+                                        z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+  const double hz = 0.5 * z;
+  const double w = 1.0 - hz;
+  const double ca = w + (((1.0 - w) - hz) + z * cr);
+  const int q = ((int)n) & 3;                        // pi x = q*pi/2 + a
+  const double s0 = (q & 1) ? ca : sa;
+  const double c0 = (q & 1) ? sa : ca;
+  sn = (q & 2) ? -s0 : s0;
+  cs = ((q + 1) & 2) ? -c0 : c0;
+}
+
 // Two independent N(0,1) from one Philox block (fp64 Box–Muller).
 __device__ __forceinline__ void normal_pair(uint4 r, double& z0, double& z1) {
   const double u1 = u53_open0(r.x, r.y);
   const double u2 = u53(r.z, r.w);
-  const double rad = sqrt(-2.0 * log(u1));
+  const double rad = fast_sqrt(-2.0 * fast_log(u1));
   double s, c;
-  sincospi(2.0 * u2, &s, &c);
+  fast_sincospi(2.0 * u2, s, c);
   z0 = rad * c;
   z1 = rad * s;
 }

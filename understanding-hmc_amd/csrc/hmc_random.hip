@@ -16,6 +16,8 @@
 // once per launch.  The arithmetic is fp64 VALU; EXACT mode keeps the reference's operation
 // order with no FMA contraction (built with -ffp-contract=off), so for diagonal targets the
 // sampled states are bit-identical to the NumPy reference on replayed streams.
+#include <cstdlib>
+
 #include "hmc_device.hpp"
 #include "hmc_internal.hpp"
 
@@ -100,6 +102,8 @@ template <int K, bool GEN>
 __device__ __forceinline__ double chain_energy(const RandArgs& a, const Lane& ln, const int (&kk)[K],
                                                const bool (&pv)[K], const double (&q)[2 * K],
                                                const double (&p)[2 * K]) {
+  // E = V + K = 0.5*(logdet_const + (q-q0)^T P (q-q0)) + p^T Minv p / 2  (utils.py:218, samplers.py:817),
+  // summed as one group reduction of the per-coordinate terms.
   double maha = 0.0, kin = 0.0;
 #pragma unroll
   for (int j = 0; j < K; ++j) {
@@ -109,9 +113,8 @@ __device__ __forceinline__ double chain_energy(const RandArgs& a, const Lane& ln
       if (d + 1 < a.D) energy_terms<GEN>(dim_const<GEN>(a, d + 1), q[2 * j + 1], p[2 * j + 1], maha, kin);
     }
   }
-  maha = group_sum(maha, ln.s, a.lpc, ln.base);
-  kin = group_sum(kin, ln.s, a.lpc, ln.base);
-  return 0.5 * (a.logc + maha) + kin / 2.0;  // V (utils.py:218, scipy form) + K (samplers.py:817)
+  const double tot = group_sum(maha + kin, ln.s, a.lpc, ln.base);
+  return 0.5 * (a.logc + tot);
 }
 
 template <int K, bool GEN, bool REPLAY>
@@ -193,6 +196,8 @@ __global__ __launch_bounds__(256) void k_random_iters(RandArgs a) {
   }
   double Eprev = ln.active ? a.Eprev[ln.c] : 0.0;
   unsigned long long n_acc = 0, n_acc_wu = 0, n_lf = 0, n_lf2 = 0, n_oob = 0;
+  int it_base = a.it0 - a.lpc, draw_L = 0;     // cached (L, log u) draws (Philox mode)
+  double draw_lnu = 0.0;
 
   for (int it = a.it0; it < a.it1; ++it) {
     // ---- momentum resample (samplers.py:431) and initial energy (:434)
@@ -214,9 +219,17 @@ __global__ __launch_bounds__(256) void k_random_iters(RandArgs a) {
       L = ln.active ? a.rL[ln.c * (int64_t)a.niter + (it - 1)] : 0;
       lnu = ln.active ? a.rlnu[ln.c * (int64_t)a.niter + (it - 1)] : 0.0;
     } else {
-      const uint4 r = draw_block(kDrawSlot, (uint32_t)it, gc, a.k0, a.k1);
-      L = ln.active ? uniform_int(r.x, a.L_low, a.L_high) : 0;
-      lnu = log(u53(r.z, r.w));
+      // lane s of the group draws (L, u) of iteration it_base + s once per LPC iterations;
+      // iteration it reads them from lane base + (it - it_base)
+      if (it - it_base >= a.lpc) {
+        it_base = it;
+        const uint4 r = draw_block(kDrawSlot, (uint32_t)(it + ln.s), gc, a.k0, a.k1);
+        draw_L = uniform_int(r.x, a.L_low, a.L_high);
+        draw_lnu = log(u53(r.z, r.w));
+      }
+      L = __shfl(draw_L, ln.base + (it - it_base), kWave);
+      lnu = __shfl(draw_lnu, ln.base + (it - it_base), kWave);
+      if (!ln.active) L = 0;
     }
 
     // ---- chain-0 trajectory capture (samplers.py:442-452): lane holding dims 0,1 records q[:2]
@@ -386,6 +399,12 @@ static double expected_max(int lo, int hi, int c) {
 Layout choose_layout(int D, int L_low, int L_high) {
   static const int Ks[] = {1, 2, 4, 5, 8, 16};
   Layout best{0, 0, 0, (D + 1) / 2};
+  if (const char* fk = getenv("HMC_FORCE_K")) {   // experiments: force the pairs-per-lane template
+    const int K = atoi(fk);
+    const int lpc = (best.npairs + K - 1) / K;
+    for (int k : Ks)
+      if (k == K && lpc <= kWave) return Layout{K, lpc, kWave / lpc, best.npairs};
+  }
   double best_score = -1.0;
   const double mean = 0.5 * (L_low + L_high - 1);
   for (int K : Ks) {
