@@ -246,4 +246,4 @@ def test_philox_normals_match_numpy_box_muller():
     z1 = r * np.sin(2 * np.pi * u2)
     ref = np.stack([z0, z1], axis=1).reshape(n, npairs, 2)
     err = np.abs(got - ref) / (r.reshape(n, npairs, 1) + 1e-300)
-    assert err.max() < 2e-15, err.max()
+    assert err.max() < 4e-15, err.max()

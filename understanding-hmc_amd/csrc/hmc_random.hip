@@ -198,6 +198,10 @@ __global__ __launch_bounds__(256) void k_random_iters(RandArgs a) {
   unsigned long long n_acc = 0, n_acc_wu = 0, n_lf = 0, n_lf2 = 0, n_oob = 0;
   int it_base = a.it0 - a.lpc, draw_L = 0;     // cached (L, log u) draws (Philox mode)
   double draw_lnu = 0.0;
+  // Retire the state loads here: the wait-count pass otherwise sees them pending at the loop
+  // header and emits vmcnt(0) inside the loop, which (loads and stores share one in-order
+  // counter on gfx950) stalls every iteration on the previous iteration's sample stores.
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) only
 
   for (int it = a.it0; it < a.it1; ++it) {
     // ---- momentum resample (samplers.py:431) and initial energy (:434)
@@ -207,8 +211,8 @@ __global__ __launch_bounds__(256) void k_random_iters(RandArgs a) {
     const bool write_row = post && ((it == a.niter) || ((it - a.wu + 1) % a.thin == 0));
     const int64_t row = post ? (int64_t)((it - a.wu) / a.thin) : 0;
     if (ln.leader && write_row) {                       // :436-438 (Q14)
-      if (a.Ec) a.Ec[ln.c * (int64_t)a.Lc + row] = E0;
-      if (a.dEc) a.dEc[ln.c * (int64_t)a.Lc + row] = E0 - Eprev;
+      __builtin_nontemporal_store(E0, a.Ec + ln.c * (int64_t)a.Lc + row);
+      __builtin_nontemporal_store(E0 - Eprev, a.dEc + ln.c * (int64_t)a.Lc + row);
     }
     Eprev = E0;                                          // :460
 
