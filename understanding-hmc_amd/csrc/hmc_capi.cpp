@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "hmc.h"
@@ -13,6 +14,8 @@
 namespace {
 
 thread_local std::string g_err;
+unsigned long long* g_stamps = nullptr;   // HMC_DEBUG_STAMPS diagnostic buffer
+int64_t g_stamp_waves = 0;
 
 hmc_status fail(hmc_status st, const char* fmt, ...) {
   char buf[512];
@@ -93,6 +96,14 @@ hmc::RandArgs rand_args(const hmc_target* t, const hmc_kinetic* k, const hmc_sch
   a.Ec = st->E_chain;
   a.dEc = st->dE_chain;
   a.cnt = st->counters;
+  if (const char* ab = getenv("HMC_DEBUG_ABLATE")) a.dbg = atoi(ab);   // profiling experiments only
+  if (getenv("HMC_DEBUG_STAMPS")) {                                     // diagnostic phase timers
+    const int64_t waves = (s->n_chains + lay.cpw - 1) / lay.cpw;
+    if (g_stamps) (void)hipFree(g_stamps);
+    g_stamps = nullptr;
+    g_stamp_waves = waves;
+    if (hipMalloc(&g_stamps, waves * 8 * sizeof(unsigned long long)) == hipSuccess) a.stamps = g_stamps;
+  }
   if (st->traj_q && st->traj_len && st->decision && st->n_save > 0) {
     a.traj_q = st->traj_q;
     a.traj_len = st->traj_len;
@@ -110,6 +121,15 @@ bool general_diag(const hmc_target* t, const hmc_kinetic* k) {
 }  // namespace
 
 extern "C" {
+
+// Diagnostic: copy the per-wave phase timers of the last HMC_DEBUG_STAMPS launch (not in hmc.h).
+int64_t hmc_debug_stamps(unsigned long long* host, int64_t cap_words) {
+  if (!g_stamps) return 0;
+  const int64_t words = g_stamp_waves * 8 < cap_words ? g_stamp_waves * 8 : cap_words;
+  if (hipDeviceSynchronize() != hipSuccess) return 0;
+  if (hipMemcpy(host, g_stamps, words * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  return words;
+}
 
 const char* hmc_version(void) { return "hmc_amd 0.1.0 gfx950 (diag random kernels, C ABI v1)"; }
 

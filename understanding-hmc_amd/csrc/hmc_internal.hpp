@@ -43,6 +43,8 @@ struct RandArgs {
   int32_t* traj_len;
   int32_t* decision;
   int n_save, traj_stride;
+  int dbg;               // ablation flags (HMC_DEBUG_ABLATE env; 0 in normal runs)
+  unsigned long long* stamps;  // diagnostic phase timers (HMC_DEBUG_STAMPS env; null in normal runs)
 };
 
 // Dense-precision (correlated MVN) Random-trajectory kernel arguments.

@@ -78,6 +78,10 @@ __device__ __forceinline__ void energy_terms(const DimConst& c, double q, double
   }
 }
 
+__device__ __forceinline__ unsigned long long stamp(bool on) {
+  return on ? __builtin_amdgcn_s_memtime() : 0ull;
+}
+
 struct Lane {
   int lane, g, s, base;
   int64_t c;       // local chain index
@@ -181,6 +185,7 @@ __global__ __launch_bounds__(256) void k_random_init(RandArgs a) {
 // Iterations [it0, it1) (samplers.py:428-475).
 template <int K, bool EXACT, bool GEN, bool REPLAY>
 __global__ __launch_bounds__(256) void k_random_iters(RandArgs a) {
+  const unsigned long long t_start = stamp(a.stamps != nullptr);
   const Lane ln = lane_info(a);
   const bool even = (a.D & 1) == 0;
   const uint64_t gc = (uint64_t)(a.chain_offset + ln.c);
@@ -198,6 +203,7 @@ __global__ __launch_bounds__(256) void k_random_iters(RandArgs a) {
   unsigned long long n_acc = 0, n_acc_wu = 0, n_lf = 0, n_lf2 = 0, n_oob = 0;
   int it_base = a.it0 - a.lpc, draw_L = 0;     // cached (L, log u) draws (Philox mode)
   double draw_lnu = 0.0;
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};   // diagnostic phase timers (stamps build path)
   // Retire the state loads here: the wait-count pass otherwise sees them pending at the loop
   // header and emits vmcnt(0) inside the loop, which (loads and stores share one in-order
   // counter on gfx950) stalls every iteration on the previous iteration's sample stores.
@@ -205,12 +211,21 @@ __global__ __launch_bounds__(256) void k_random_iters(RandArgs a) {
 
   for (int it = a.it0; it < a.it1; ++it) {
     // ---- momentum resample (samplers.py:431) and initial energy (:434)
-    draw_momentum<K, GEN, REPLAY>(a, ln, it, kk, pv, p);
-    const double E0 = chain_energy<K, GEN>(a, ln, kk, pv, q, p);
+    const bool st_on = a.stamps != nullptr;
+    unsigned long long t_0 = stamp(st_on);
+    if (!(a.dbg & 1)) {
+      draw_momentum<K, GEN, REPLAY>(a, ln, it, kk, pv, p);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 2 * K; ++e) p[e] = 0.3;
+    }
+    unsigned long long t_1 = stamp(st_on);
+    const double E0 = (a.dbg & 2) ? 0.0 : chain_energy<K, GEN>(a, ln, kk, pv, q, p);
+    unsigned long long t_2 = stamp(st_on);
     const bool post = it >= a.wu;
     const bool write_row = post && ((it == a.niter) || ((it - a.wu + 1) % a.thin == 0));
     const int64_t row = post ? (int64_t)((it - a.wu) / a.thin) : 0;
-    if (ln.leader && write_row) {                       // :436-438 (Q14)
+    if (ln.leader && write_row && !(a.dbg & 8)) {       // :436-438 (Q14)
       __builtin_nontemporal_store(E0, a.Ec + ln.c * (int64_t)a.Lc + row);
       __builtin_nontemporal_store(E0 - Eprev, a.dEc + ln.c * (int64_t)a.Lc + row);
     }
@@ -233,9 +248,12 @@ __global__ __launch_bounds__(256) void k_random_iters(RandArgs a) {
       }
       L = __shfl(draw_L, ln.base + (it - it_base), kWave);
       lnu = __shfl(draw_lnu, ln.base + (it - it_base), kWave);
+      if (a.dbg & 16) L = 12;
+      if (a.dbg & 4) L = 0;
       if (!ln.active) L = 0;
     }
 
+    unsigned long long t_3 = stamp(st_on);
     // ---- chain-0 trajectory capture (samplers.py:442-452): lane holding dims 0,1 records q[:2]
     const bool cap = a.traj_q && (gc == 0) && (it <= a.n_save) && ln.leader;
     double* capp = cap ? a.traj_q + (int64_t)(it - 1) * a.traj_stride * 2 : nullptr;
@@ -301,15 +319,17 @@ __global__ __launch_bounds__(256) void k_random_iters(RandArgs a) {
       }
     }
 
+    unsigned long long t_4 = stamp(st_on);
     // ---- final energy and Metropolis test (:455-472)
-    const double E1 = chain_energy<K, GEN>(a, ln, kk, pv, q, p);
+    const double E1 = (a.dbg & 2) ? 0.0 : chain_energy<K, GEN>(a, ln, kk, pv, q, p);
+    unsigned long long t_5 = stamp(st_on);
     const double dE = E1 - E0;
     const bool accept = (dE < 0.0) || (lnu < -dE);
     if (!accept) {
 #pragma unroll
       for (int e = 0; e < 2 * K; ++e) q[e] = qi[e];
     }
-    if (write_row && a.qc) {
+    if (write_row && a.qc && !(a.dbg & 8)) {
       double* rowp = a.qc + (ln.c * (int64_t)a.Lc + row) * a.D;
 #pragma unroll
       for (int j = 0; j < K; ++j)
@@ -329,6 +349,15 @@ __global__ __launch_bounds__(256) void k_random_iters(RandArgs a) {
       n_lf += Lp;
       n_lf2 += Lp * Lp;
     }
+    if (st_on) {
+      const unsigned long long t_6 = stamp(true);
+      ph[0] += t_1 - t_0;   // momentum draw
+      ph[1] += t_2 - t_1;   // E0
+      ph[2] += t_3 - t_2;   // row bookkeeping + L/u draw
+      ph[3] += t_4 - t_3;   // leapfrog loop
+      ph[4] += t_5 - t_4;   // E1
+      ph[5] += t_6 - t_5;   // MH + stores
+    }
   }
 
   // ---- state write-back and counters
@@ -336,6 +365,18 @@ __global__ __launch_bounds__(256) void k_random_iters(RandArgs a) {
   for (int j = 0; j < K; ++j)
     if (pv[j]) store_pair(a.q + ln.c * (int64_t)a.D, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);
   if (ln.leader) a.Eprev[ln.c] = Eprev;
+  if (a.stamps && ln.lane == 0) {
+    const int64_t wv = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) a.stamps[wv * 8 + i] = ph[i];
+    a.stamps[wv * 8 + 6] = t_start;
+    a.stamps[wv * 8 + 7] = stamp(true);
+    // hardware placement: HW_ID (wave/simd/cu/sh/se) in the high word of slot 5's neighbour
+    const unsigned hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    a.stamps[wv * 8 + 5] = ((unsigned long long)hwid << 32) | ((unsigned long long)(xcc & 0xffff) << 16) |
+                           (a.stamps[wv * 8 + 5] & 0xffffull);
+  }
   n_acc = wave_sum_u64(n_acc);
   n_acc_wu = wave_sum_u64(n_acc_wu);
   n_lf = wave_sum_u64(n_lf);
