@@ -37,6 +37,7 @@ def parse():
     ap.add_argument("--iters-per-step", type=int, default=10)
     ap.add_argument("--fp-mode", default="fast", choices=["fast", "exact"])
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--dt", type=float, default=0.1)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget per process")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ess", action="store_true")
@@ -121,7 +122,7 @@ def main():
     n_iter = (W + K) * S
     wu = W * S + 1                     # q_chain rows 0..K*S hold exactly the timed iterations
     tgt = MVNTarget(np.zeros(D), np.eye(D))
-    eng = RandomEngine(tgt, N, n_iter, wu, 1, 5, 20, 0.1, rng="philox", seed=a.seed, fp_mode=a.fp_mode,
+    eng = RandomEngine(tgt, N, n_iter, wu, 1, 5, 20, a.dt, rng="philox", seed=a.seed, fp_mode=a.fp_mode,
                        chain_offset=rank * N, store_chain=not a.no_ess, device=dev)
     rs = np.random.RandomState(a.seed + rank)
     eng.init(torch.as_tensor(rs.standard_normal((N, D)) * np.sqrt(2.0), device=dev))

@@ -52,7 +52,10 @@ enum {
   HMC_CNT_UNSTABLE = 5,      /* NUTS |E-E0| > 1000 sub-tree rejections (samplers.py:647)     */
   HMC_CNT_DMAX = 6,          /* NUTS chain-iterations that hit d_max                         */
   HMC_CNT_ENERGY_EVALS = 7,  /* NUTS energy evaluations (N_total_steps accounting)           */
-  HMC_NCOUNTERS = 8
+  HMC_NCOUNTERS = 8,
+  /* counters are spread over HMC_COUNTER_SLOTS rows ([slot][HMC_NCOUNTERS]) so that the
+   * per-wave atomics of a launch do not serialise on one address; totals = sum over slots */
+  HMC_COUNTER_SLOTS = 4096
 };
 
 /* MVN target: V(q) = 0.5*(logdet_const + (q-q0)^T P (q-q0)), dV/dq = P (q-q0).
@@ -115,7 +118,7 @@ typedef struct hmc_state {
   double* q_chain;         /* [n_chains][L_chain][D] or NULL (no sample storage)          */
   double* E_chain;         /* [n_chains][L_chain] or NULL                                  */
   double* dE_chain;        /* [n_chains][L_chain] or NULL                                  */
-  unsigned long long* counters; /* [HMC_NCOUNTERS]                                          */
+  unsigned long long* counters; /* [HMC_COUNTER_SLOTS][HMC_NCOUNTERS], zero-initialised       */
   /* Trajectory capture of global chain 0 for the first n_save iterations (make_movie input;
    * samplers.py:397-400, :442-475): traj_q[n_save][traj_stride][2] = q[:2] after each step,
    * traj_len[n_save] = L+1, decision[n_save] = accepted.  NULL / 0 disables capture. */

@@ -97,6 +97,8 @@ hmc::RandArgs rand_args(const hmc_target* t, const hmc_kinetic* k, const hmc_sch
   a.dEc = st->dE_chain;
   a.cnt = st->counters;
   if (const char* ab = getenv("HMC_DEBUG_ABLATE")) a.dbg = atoi(ab);   // profiling experiments only
+  a.dbgL = -1;
+  if (const char* dl = getenv("HMC_DEBUG_L")) a.dbgL = atoi(dl);
   if (getenv("HMC_DEBUG_STAMPS")) {                                     // diagnostic phase timers
     const int64_t waves = (s->n_chains + lay.cpw - 1) / lay.cpw;
     if (g_stamps) (void)hipFree(g_stamps);

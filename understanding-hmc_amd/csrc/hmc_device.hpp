@@ -172,4 +172,33 @@ __device__ __forceinline__ void store_pair(double* __restrict__ row, int k, bool
   }
 }
 
+// ---- full-wave fp64 sum with DPP (no LDS traffic): row_shr 1/2/4/8 prefix inside each
+// 16-lane row, then row_bcast15 / row_bcast31 fold the rows; lane 63 holds the total, which
+// v_readlane turns into a wave-uniform (SGPR) value.  EXEC must be all ones at the call.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ double dpp0(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW_MASK, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp0<0x111>(v);        // row_shr:1
+  v += dpp0<0x112>(v);        // row_shr:2
+  v += dpp0<0x114>(v);        // row_shr:4
+  v += dpp0<0x118>(v);        // row_shr:8
+  v += dpp0<0x142, 0xA>(v);   // row_bcast:15 -> rows 1, 3
+  v += dpp0<0x143, 0xC>(v);   // row_bcast:31 -> rows 2, 3
+  return readlane_d(v, 63);
+}
+
+__device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ double uniform_d(double v) { return readlane_d(v, 0); }
+
 }  // namespace hmc

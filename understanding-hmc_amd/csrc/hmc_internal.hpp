@@ -44,6 +44,7 @@ struct RandArgs {
   int32_t* decision;
   int n_save, traj_stride;
   int dbg;               // ablation flags (HMC_DEBUG_ABLATE env; 0 in normal runs)
+  int dbgL;              // forced trajectory length (HMC_DEBUG_L env; -1 in normal runs)
   unsigned long long* stamps;  // diagnostic phase timers (HMC_DEBUG_STAMPS env; null in normal runs)
 };
 
@@ -77,6 +78,7 @@ Layout choose_layout(int D, int L_low, int L_high);
 hipError_t launch_random_init(const RandArgs& a, const Layout& lay, bool gen, bool replay, hipStream_t s);
 hipError_t launch_random_iters(const RandArgs& a, const Layout& lay, bool exact, bool gen, bool replay,
                                hipStream_t s);
+hipError_t launch_wave_iters(const RandArgs& a, int K, bool exact, bool gen, bool replay, hipStream_t s);
 hipError_t launch_dense_init(const DenseArgs& a, bool replay, hipStream_t s);
 hipError_t launch_dense_iters(const DenseArgs& a, bool exact, bool replay, hipStream_t s);
 

@@ -20,63 +20,11 @@
 
 #include "hmc_device.hpp"
 #include "hmc_internal.hpp"
+#include "hmc_target_ops.hpp"
 
 namespace hmc {
 
 namespace {
-
-// Per-dimension constants of the general diagonal target (loaded through L1/L2; tiny).
-struct DimConst {
-  double q0, prec, minv, dt, hd;
-};
-
-template <bool GEN>
-__device__ __forceinline__ DimConst dim_const(const RandArgs& a, int d) {
-  DimConst c{0.0, 1.0, 1.0, a.dt, a.h};
-  if constexpr (GEN) {
-    if (a.q0) c.q0 = a.q0[d];
-    if (a.prec) c.prec = a.prec[d];
-    if (a.minv) c.minv = a.minv[d];
-    if (a.dtv) {
-      c.dt = a.dtv[d];
-      c.hd = c.dt * 0.5;
-    }
-  }
-  return c;
-}
-
-// Constants of coordinate slot (pair k, half h); padding slots get neutral constants and never
-// touch the per-dimension arrays.
-template <bool GEN>
-__device__ __forceinline__ DimConst slot_const(const RandArgs& a, int k, int h, bool pair_valid) {
-  const int d = 2 * k + h;
-  if (GEN && pair_valid && d < a.D) return dim_const<GEN>(a, d);
-  return DimConst{0.0, 1.0, 1.0, a.dt, a.h};
-}
-
-// Kick term (dt * (Minv * (P (q - q0)))) / 2 in the reference's operation order
-// (samplers.py:835/:837 with dVdq of case1-script.py:49).  (dt*x)/2 == (dt/2)*x exactly.
-template <bool GEN>
-__device__ __forceinline__ double kick(const DimConst& c, double q) {
-  if constexpr (GEN) {
-    return c.hd * (c.minv * (c.prec * (q - c.q0)));
-  } else {
-    return c.hd * q;
-  }
-}
-
-template <bool GEN>
-__device__ __forceinline__ void energy_terms(const DimConst& c, double q, double p, double& maha,
-                                             double& kin) {
-  if constexpr (GEN) {
-    const double x = q - c.q0;
-    maha += c.prec * x * x;
-    kin += p * (c.minv * p);
-  } else {
-    maha += q * q;
-    kin += p * p;
-  }
-}
 
 __device__ __forceinline__ unsigned long long stamp(bool on) {
   return on ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -382,12 +330,14 @@ __global__ __launch_bounds__(256) void k_random_iters(RandArgs a) {
   n_lf = wave_sum_u64(n_lf);
   n_lf2 = wave_sum_u64(n_lf2);
   n_oob = wave_sum_u64(n_oob);
-  if (ln.lane == 0 && a.cnt) {
-    if (n_acc) atomicAdd(a.cnt + HMC_CNT_ACCEPT, n_acc);
-    if (n_acc_wu) atomicAdd(a.cnt + HMC_CNT_ACCEPT_WU, n_acc_wu);
-    if (n_lf) atomicAdd(a.cnt + HMC_CNT_LEAPFROG, n_lf);
-    if (n_lf2) atomicAdd(a.cnt + HMC_CNT_LEAPFROG_SQ, n_lf2);
-    if (n_oob) atomicAdd(a.cnt + HMC_CNT_OOB_REJECT, n_oob);
+  if (ln.lane == 0 && a.cnt) {   // per-wave counts into one of HMC_COUNTER_SLOTS rows
+    const int64_t wv = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+    unsigned long long* cs = a.cnt + (wv & (HMC_COUNTER_SLOTS - 1)) * HMC_NCOUNTERS;
+    if (n_acc) atomicAdd(cs + HMC_CNT_ACCEPT, n_acc);
+    if (n_acc_wu) atomicAdd(cs + HMC_CNT_ACCEPT_WU, n_acc_wu);
+    if (n_lf) atomicAdd(cs + HMC_CNT_LEAPFROG, n_lf);
+    if (n_lf2) atomicAdd(cs + HMC_CNT_LEAPFROG_SQ, n_lf2);
+    if (n_oob) atomicAdd(cs + HMC_CNT_OOB_REJECT, n_oob);
   }
 }
 
@@ -450,6 +400,15 @@ Layout choose_layout(int D, int L_low, int L_high) {
     for (int k : Ks)
       if (k == K && lpc <= kWave) return Layout{K, lpc, kWave / lpc, best.npairs};
   }
+  // D > 64: one wavefront per chain (hmc_wave.hip): no trajectory-length divergence inside a
+  // wave, wave-uniform control flow; K pairs per lane.
+  if (best.npairs > kWave / 2) {
+    for (int K : {1, 2, 4, 8, 16})
+      if (K * kWave >= best.npairs) return Layout{K, kWave, 1, best.npairs};
+    return best;  // K = 0: unsupported
+  }
+  // small D: several chains per wave (lane groups); pick K by lane utilisation discounted by the
+  // expected trajectory-length divergence between the chains sharing a wave
   double best_score = -1.0;
   const double mean = 0.5 * (L_low + L_high - 1);
   for (int K : Ks) {
@@ -484,6 +443,10 @@ hipError_t launch_random_init(const RandArgs& a, const Layout& lay, bool gen, bo
 
 hipError_t launch_random_iters(const RandArgs& a, const Layout& lay, bool exact, bool gen, bool replay,
                                hipStream_t s) {
+  const char* kern = getenv("HMC_KERNEL");       // experiments: "group" forces the lane-group kernel
+  if (lay.cpw == 1 && !(kern && kern[0] == 'g') && (lay.K == 1 || lay.K == 2 || lay.K == 4 || lay.K == 8 ||
+                                                  lay.K == 16))
+    return launch_wave_iters(a, lay.K, exact, gen, replay, s);
   const dim3 grid = grid_for(a);
   switch (lay.K) {
     case 1: return launch_iters_k<1>(a, exact, gen, replay, grid, s);

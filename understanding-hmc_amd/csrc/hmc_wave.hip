@@ -1,0 +1,329 @@
+// hmc_wave.hip — wave-per-chain Random-trajectory HMC kernel (diagonal-precision MVN, D > 64).
+//
+// Same semantics as k_random_iters (hmc_random.hip; samplers.py:428-475) with the layout the
+// north star asks for: ONE wavefront per chain.  Lane l owns coordinate pairs l + 64*j.
+// Everything that is per chain is wave-uniform, which the kernel exploits:
+//   * trajectory length L and the MH log-uniform are SGPR values, so the leapfrog loop is a
+//     scalar loop (no EXEC juggling) and the accept/reject is a scalar branch;
+//   * energies are full-wave DPP reductions (row_shr/row_bcast, no LDS), read back with
+//     v_readlane as SGPRs;
+//   * one reduction per iteration: the final energy E1 of iteration i is reduced together
+//     with the kinetic energy of iteration i+1's momentum (drawn before the MH test, its
+//     draw is keyed by i+1 so the order of work does not change any value), and the potential
+//     part of E0(i+1) is V(q) already known from E1 (accepted) or E0 (rejected);
+//   * E_chain / dE_chain values of up to 64 iterations are parked one per lane and written
+//     as one coalesced store (rows of a chain are contiguous).
+// HBM traffic per chain-iteration: one q_chain row (8D B) + E + dE (16 B).
+#include "hmc_device.hpp"
+#include "hmc_internal.hpp"
+#include "hmc_target_ops.hpp"
+
+namespace hmc {
+
+namespace {
+
+template <int K, bool GEN>
+__device__ __forceinline__ void wave_partials(const RandArgs& a, const int (&kk)[K], const bool (&pv)[K],
+                                              const double (&q)[2 * K], const double (&p)[2 * K], double& maha,
+                                              double& kin) {
+  maha = 0.0;
+  kin = 0.0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    if (pv[j]) {
+      const int d = 2 * kk[j];
+      energy_terms<GEN>(dim_const<GEN>(a, d), q[2 * j], p[2 * j], maha, kin);
+      if (d + 1 < a.D) energy_terms<GEN>(dim_const<GEN>(a, d + 1), q[2 * j + 1], p[2 * j + 1], maha, kin);
+    }
+  }
+}
+
+template <int K, bool GEN>
+__device__ __forceinline__ double kin_partial(const RandArgs& a, const int (&kk)[K], const bool (&pv)[K],
+                                              const double (&p)[2 * K]) {
+  double kin = 0.0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    if (pv[j]) {
+      const int d = 2 * kk[j];
+      const DimConst c0 = dim_const<GEN>(a, d);
+      kin += GEN ? p[2 * j] * (c0.minv * p[2 * j]) : p[2 * j] * p[2 * j];
+      if (d + 1 < a.D) {
+        const DimConst c1 = dim_const<GEN>(a, d + 1);
+        kin += GEN ? p[2 * j + 1] * (c1.minv * p[2 * j + 1]) : p[2 * j + 1] * p[2 * j + 1];
+      }
+    }
+  }
+  return kin;
+}
+
+template <int K, bool GEN, bool REPLAY>
+__device__ __forceinline__ void wave_momentum(const RandArgs& a, int64_t c, uint64_t gc, int it, const int (&kk)[K],
+                                              const bool (&pv)[K], double (&p)[2 * K]) {
+  const bool even = (a.D & 1) == 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    p[2 * j] = 0.0;
+    p[2 * j + 1] = 0.0;
+    if (pv[j]) {
+      const int d = 2 * kk[j];
+      if constexpr (REPLAY) {
+        const double* row = a.rp + (c * (int64_t)a.niter + (it - 1)) * a.D;
+        load_pair(row, kk[j], even, d + 1 < a.D, p[2 * j], p[2 * j + 1]);
+      } else {
+        normal_pair(draw_block((uint32_t)kk[j], (uint32_t)it, gc, a.k0, a.k1), p[2 * j], p[2 * j + 1]);
+        if (GEN && a.pscale) {
+          p[2 * j] *= a.pscale[d];
+          if (d + 1 < a.D) p[2 * j + 1] *= a.pscale[d + 1];
+        }
+      }
+      if (d + 1 >= a.D) p[2 * j + 1] = 0.0;
+    }
+  }
+}
+
+template <int K, bool EXACT, bool GEN, bool REPLAY>
+__global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t c = uniform_i(blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave));
+  if (c >= a.n) return;                                  // whole wave, uniform
+  const uint64_t gc = (uint64_t)(a.chain_offset + c);
+  const bool even = (a.D & 1) == 0;
+  int kk[K];
+  bool pv[K];
+  double q[2 * K], p[2 * K], qi[2 * K], pn[2 * K];
+  double* const qrow = a.q + c * (int64_t)a.D;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    kk[j] = lane + kWave * j;
+    pv[j] = kk[j] < a.npairs;
+    q[2 * j] = q[2 * j + 1] = 0.0;
+    if (pv[j]) load_pair(qrow, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);
+  }
+  double Eprev = a.Eprev[c];
+  __builtin_amdgcn_s_waitcnt(0x0F70);                    // retire state loads before the loop (vmcnt(0))
+
+  // momentum and energy of the first iteration of this launch
+  wave_momentum<K, GEN, REPLAY>(a, c, gc, a.it0, kk, pv, p);
+  double m0, k0;
+  wave_partials<K, GEN>(a, kk, pv, q, p, m0, k0);
+  m0 = wave_sum_dpp(m0);
+  k0 = wave_sum_dpp(k0);
+  double E0 = 0.5 * (a.logc + (m0 + k0));
+
+  // thinning bookkeeping without divisions: row = (it - wu)//thin, phase = (it - wu) % thin
+  int row = 0, phase = 0;
+  if (a.it0 >= a.wu) {
+    row = (a.it0 - a.wu) / a.thin;
+    phase = (a.it0 - a.wu) - row * a.thin;
+  }
+  double Ebuf = 0.0, dEbuf = 0.0;
+  int rowbuf = -1, nbuf = 0;
+  double* const Ec = a.Ec ? a.Ec + c * (int64_t)a.Lc : nullptr;
+  double* const dEc = a.dEc ? a.dEc + c * (int64_t)a.Lc : nullptr;
+  double* const qcb = a.qc ? a.qc + c * (int64_t)a.Lc * a.D : nullptr;
+  const bool cap_chain = a.traj_q && gc == 0 && !(a.dbg & 32);
+  unsigned long long n_acc = 0, n_acc_wu = 0, n_lf = 0, n_lf2 = 0, n_oob = 0;
+  int it_base = a.it0 - kWave, draw_L = 0;
+  double draw_lnu = 0.0;
+
+  for (int it = a.it0; it < a.it1; ++it) {
+    const bool post = it >= a.wu;
+    const bool write_row = post && ((it == a.niter) || (phase == a.thin - 1));
+    // E_chain / dE_chain of this iteration parked in lane nbuf (flushed every 64 or at the end)
+    if (write_row) {
+      if (lane == nbuf) {
+        Ebuf = E0;
+        dEbuf = E0 - Eprev;
+        rowbuf = row;
+      }
+      if (++nbuf == kWave) {
+        if (rowbuf >= 0) {
+          if (Ec) __builtin_nontemporal_store(Ebuf, Ec + rowbuf);
+          if (dEc) __builtin_nontemporal_store(dEbuf, dEc + rowbuf);
+        }
+        rowbuf = -1;
+        nbuf = 0;
+      }
+    }
+    Eprev = E0;
+
+    // trajectory length (:441) and MH log-uniform (:461): wave-uniform
+    int L;
+    double lnu;
+    if constexpr (REPLAY) {
+      L = a.rL[c * (int64_t)a.niter + (it - 1)];
+      lnu = a.rlnu[c * (int64_t)a.niter + (it - 1)];
+    } else {
+      if (it - it_base >= kWave) {                       // lane l draws (L, u) of iteration it + l
+        it_base = it;
+        const uint4 r = draw_block(kDrawSlot, (uint32_t)(it + lane), gc, a.k0, a.k1);
+        draw_L = uniform_int(r.x, a.L_low, a.L_high);
+        draw_lnu = log(u53(r.z, r.w));
+      }
+      L = __builtin_amdgcn_readlane(draw_L, it - it_base);
+      lnu = readlane_d(draw_lnu, it - it_base);
+    }
+    if (a.dbgL >= 0) L = a.dbgL;                          // diagnostics: forced trajectory length
+    L = uniform_i(L);
+
+    // chain-0 trajectory capture (samplers.py:442-452)
+    const bool cap = cap_chain && it <= a.n_save;
+    double* capp = cap ? a.traj_q + (int64_t)(it - 1) * a.traj_stride * 2 : nullptr;
+    if (cap && lane == 0) {
+      capp[0] = q[0];
+      capp[1] = a.D > 1 ? q[1] : q[0];
+    }
+
+    // L leapfrog steps (samplers.py:448 -> :831-839), scalar loop
+#pragma unroll
+    for (int e = 0; e < 2 * K; ++e) qi[e] = q[e];
+    if constexpr (EXACT) {
+      double t[2 * K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) t[2 * j + h] = kick<GEN>(slot_const<GEN>(a, kk[j], h, pv[j]), q[2 * j + h]);
+      }
+      for (int l = 0; l < L; ++l) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int e = 2 * j + h;
+            const DimConst cc = slot_const<GEN>(a, kk[j], h, pv[j]);
+            const double ph = p[e] - t[e];
+            q[e] = q[e] + cc.dt * ph;
+            t[e] = kick<GEN>(cc, q[e]);
+            p[e] = ph - t[e];
+          }
+        }
+        if (cap && lane == 0) {
+          capp[2 * (l + 1)] = q[0];
+          capp[2 * (l + 1) + 1] = a.D > 1 ? q[1] : q[0];
+        }
+      }
+    } else {
+      for (int l = 0; l < L; ++l) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int e = 2 * j + h;
+            const DimConst cc = slot_const<GEN>(a, kk[j], h, pv[j]);
+            const double co = GEN ? cc.hd * (cc.minv * cc.prec) : cc.hd;
+            const double ph = __builtin_fma(-co, q[e] - cc.q0, p[e]);
+            q[e] = __builtin_fma(cc.dt, ph, q[e]);
+            p[e] = __builtin_fma(-co, q[e] - cc.q0, ph);
+          }
+        }
+        if (cap && lane == 0) {
+          capp[2 * (l + 1)] = q[0];
+          capp[2 * (l + 1) + 1] = a.D > 1 ? q[1] : q[0];
+        }
+      }
+    }
+
+    // next iteration's momentum (keyed by it+1) so its kinetic energy joins this reduction
+    const bool more = it + 1 < a.it1;
+    double kn = 0.0;
+    if (more && !(a.dbg & 256)) {
+      wave_momentum<K, GEN, REPLAY>(a, c, gc, it + 1, kk, pv, pn);
+      kn = kin_partial<K, GEN>(a, kk, pv, pn);
+    }
+    double m1, k1;
+    wave_partials<K, GEN>(a, kk, pv, q, p, m1, k1);
+    m1 = wave_sum_dpp(m1);
+    k1 = wave_sum_dpp(k1);
+    kn = wave_sum_dpp(kn);
+    const double E1 = 0.5 * (a.logc + (m1 + k1));
+    const double dE = E1 - E0;                            // samplers.py:459
+    const bool accept = (dE < 0.0) || (lnu < -dE);        // :462
+    if (!accept && !(a.dbg & 128)) {
+#pragma unroll
+      for (int e = 0; e < 2 * K; ++e) q[e] = qi[e];
+    }
+    if (write_row && qcb && !(a.dbg & 64)) {
+      double* rowp = qcb + (int64_t)row * a.D;
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        if (pv[j]) store_pair(rowp, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);
+    }
+    if (cap && lane == 0) {
+      a.traj_len[it - 1] = (L > 0 ? L : 0) + 1;
+      a.decision[it - 1] = accept ? 1 : 0;
+    }
+    if (accept) {
+      if (post) ++n_acc; else ++n_acc_wu;
+    } else if (it < a.i_oob) {
+      ++n_oob;
+    }
+    const unsigned long long Lp = L > 0 ? (unsigned long long)L : 0ull;
+    n_lf += Lp;
+    n_lf2 += Lp * Lp;
+    // advance
+    if (more) {
+#pragma unroll
+      for (int e = 0; e < 2 * K; ++e) p[e] = pn[e];
+      m0 = accept ? m1 : m0;
+      E0 = 0.5 * (a.logc + (m0 + kn));
+    }
+    if (post && ++phase == a.thin) {
+      phase = 0;
+      ++row;
+    }
+  }
+
+  // flush parked E/dE, write back state and counters
+  if (rowbuf >= 0) {
+    if (Ec) __builtin_nontemporal_store(Ebuf, Ec + rowbuf);
+    if (dEc) __builtin_nontemporal_store(dEbuf, dEc + rowbuf);
+  }
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+    if (pv[j]) store_pair(qrow, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);
+  if (lane == 0) {
+    a.Eprev[c] = Eprev;
+    if (a.cnt) {   // per-wave counts into one of HMC_COUNTER_SLOTS rows (no single-address hot spot)
+      unsigned long long* cs = a.cnt + (c & (HMC_COUNTER_SLOTS - 1)) * HMC_NCOUNTERS;
+      if (n_acc) atomicAdd(cs + HMC_CNT_ACCEPT, n_acc);
+      if (n_acc_wu) atomicAdd(cs + HMC_CNT_ACCEPT_WU, n_acc_wu);
+      if (n_lf) atomicAdd(cs + HMC_CNT_LEAPFROG, n_lf);
+      if (n_lf2) atomicAdd(cs + HMC_CNT_LEAPFROG_SQ, n_lf2);
+      if (n_oob) atomicAdd(cs + HMC_CNT_OOB_REJECT, n_oob);
+    }
+  }
+}
+
+template <int K, bool EXACT>
+hipError_t launch_wave_k2(const RandArgs& a, bool gen, bool replay, dim3 grid, hipStream_t s) {
+  if (gen) {
+    if (replay) k_wave_iters<K, EXACT, true, true><<<grid, 256, 0, s>>>(a);
+    else k_wave_iters<K, EXACT, true, false><<<grid, 256, 0, s>>>(a);
+  } else {
+    if (replay) k_wave_iters<K, EXACT, false, true><<<grid, 256, 0, s>>>(a);
+    else k_wave_iters<K, EXACT, false, false><<<grid, 256, 0, s>>>(a);
+  }
+  return hipGetLastError();
+}
+
+template <int K>
+hipError_t launch_wave_k(const RandArgs& a, bool exact, bool gen, bool replay, dim3 grid, hipStream_t s) {
+  return exact ? launch_wave_k2<K, true>(a, gen, replay, grid, s) : launch_wave_k2<K, false>(a, gen, replay, grid, s);
+}
+
+}  // namespace
+
+hipError_t launch_wave_iters(const RandArgs& a, int K, bool exact, bool gen, bool replay, hipStream_t s) {
+  const dim3 grid((unsigned)((a.n + 3) / 4));
+  switch (K) {
+    case 1: return launch_wave_k<1>(a, exact, gen, replay, grid, s);
+    case 2: return launch_wave_k<2>(a, exact, gen, replay, grid, s);
+    case 4: return launch_wave_k<4>(a, exact, gen, replay, grid, s);
+    case 8: return launch_wave_k<8>(a, exact, gen, replay, grid, s);
+    case 16: return launch_wave_k<16>(a, exact, gen, replay, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace hmc

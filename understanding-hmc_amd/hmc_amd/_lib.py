@@ -16,6 +16,7 @@ HMC_MODE_EXACT, HMC_MODE_FAST = 0, 1
 (CNT_ACCEPT, CNT_ACCEPT_WU, CNT_LEAPFROG, CNT_LEAPFROG_SQ, CNT_OOB_REJECT, CNT_UNSTABLE, CNT_DMAX,
  CNT_ENERGY_EVALS) = range(8)
 NCOUNTERS = 8
+COUNTER_SLOTS = 4096   # include/hmc.h HMC_COUNTER_SLOTS: counters buffer is [slots][NCOUNTERS]
 
 c_dp = ctypes.c_void_p  # device pointers are passed as integers (torch data_ptr())
 

@@ -60,7 +60,7 @@ class RandomEngine:
         self.q_chain = torch.zeros((N, Lc, D), dtype=torch.float64, device=dev) if store_chain else None
         self.E_chain = torch.zeros((N, Lc), dtype=torch.float64, device=dev) if store_energy else None
         self.dE_chain = torch.zeros((N, Lc), dtype=torch.float64, device=dev) if store_energy else None
-        self.counters = torch.zeros(H.NCOUNTERS, dtype=torch.int64, device=dev)
+        self.counters = torch.zeros((H.COUNTER_SLOTS, H.NCOUNTERS), dtype=torch.int64, device=dev)
         self.n_save = int(n_save)
         if self.n_save:
             self.traj_stride = max(self.L_high, 1)
@@ -103,4 +103,4 @@ class RandomEngine:
                                          self.stream()), "hmc_random_iters")
 
     def read_counters(self):
-        return self.counters.cpu().numpy().astype(np.int64)
+        return self.counters.cpu().numpy().astype(np.int64).sum(axis=0)
