@@ -172,7 +172,8 @@ def main():
     if rank == 0:
         # algorithmic bytes of one launch (S iterations): per chain-iteration one q_chain row +
         # E + dE (8D + 16 B); per launch q and E_prev are read and written once (16D + 16 B)
-        bytes_launch = N * (S * (8 * D + 16) + 16 * D + 16)
+        row_bytes = 8 * D if eng.q_chain is not None else 0
+        bytes_launch = N * (S * (row_bytes + 16) + 16 * D + 16)
         lf_launch = lf_local / K
         # algorithmic flops: 8D per leapfrog + 8D energies per iteration
         flops_launch = lf_launch * 8 * D + N * S * 8 * D
