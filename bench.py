@@ -38,6 +38,8 @@ def parse():
     ap.add_argument("--fp-mode", default="fast", choices=["fast", "exact"])
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--dt", type=float, default=0.1)
+    ap.add_argument("--rho", type=float, default=0.0, help="MVN correlation (0: unit/diagonal kernel; "
+                    ">0: dense precision, MFMA kernel, BASELINE config 3 uses 0.95 with 262144 chains)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget per process")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ess", action="store_true")
@@ -121,7 +123,8 @@ def main():
     W, K = a.warmup, a.steps
     n_iter = (W + K) * S
     wu = W * S + 1                     # q_chain rows 0..K*S hold exactly the timed iterations
-    tgt = MVNTarget(np.zeros(D), np.eye(D))
+    cov = np.eye(D) if a.rho == 0 else (np.diag(np.ones(D)) * (1 - a.rho) + a.rho)
+    tgt = MVNTarget(np.zeros(D), cov)
     eng = RandomEngine(tgt, N, n_iter, wu, 1, 5, 20, a.dt, rng="philox", seed=a.seed, fp_mode=a.fp_mode,
                        chain_offset=rank * N, store_chain=not a.no_ess, device=dev)
     rs = np.random.RandomState(a.seed + rank)

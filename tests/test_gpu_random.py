@@ -279,3 +279,55 @@ def test_wave_kernel_replay_exact_vs_oracle(D, thin, wu, gen):
     np.testing.assert_allclose(h.dE_chain[:, :, 0], ref["dE_chain"], rtol=1e-8, atol=1e-10)
     assert h.accept_R == ref["accept_R"]
     assert h.N_total_steps == ref["N_total_steps"]
+
+
+DENSE_FIXTURES = ["f3_case3c_small.npz", "f3b_case3a.npz", "f11_case5_unstable.npz"]
+
+
+@pytest.mark.parametrize("fx", DENSE_FIXTURES)
+@pytest.mark.parametrize("fp_mode", ["exact", "fast"])
+def test_dense_replay_matches_reference(fx, fp_mode):
+    """Correlated targets (dense inv(cov0), f64 MFMA gradient): same draws as the reference,
+    so the accept/reject sequence is identical and the states agree to round-off (the MFMA
+    k-ordered sums differ from BLAS dgemv in the last bits).  Tolerance: q_chain 1e-9 abs/rel,
+    E 1e-10 rel, R-hat / std 1e-6 rel (north-star contract)."""
+    g = load_golden(fx)
+    m = g["meta"]
+    h = _run_replay(g, fp_mode)
+    assert h.accept_R == float(g["accept_R"])
+    if m["warm_up"] > 0:
+        assert h.accept_R_warm_up == float(g["accept_R_warm_up"])
+    assert h.N_total_steps == int(g["N_total_steps"])
+    np.testing.assert_allclose(h.q_chain, g["q_chain"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(h.E_chain[:, :, 0], g["E_chain"], rtol=1e-10)
+    h.compute_convergence_stats()
+    np.testing.assert_allclose(h.R_q, g["R_q"], rtol=1e-6)
+    from hmc_amd.diagnostics import per_dim_mean_std
+    mean, std = per_dim_mean_std(h.q_chain_device)
+    np.testing.assert_allclose(std, g["std"], rtol=1e-6)
+
+
+@pytest.mark.parametrize("D,rho", [(100, 0.95), (37, 0.5), (128, 0.9)])
+def test_dense_philox_statistics(D, rho):
+    """Philox mode, dense target at scale, chains started IN the stationary law N(0, Sigma):
+    HMC leaves it invariant, so after any number of iterations the per-dim variances are 1
+    and corr(q0, q1) = rho (independent of mixing speed); results are deterministic."""
+    from hmc_amd.samplers import HMC_sampler
+    from hmc_amd.target import MVNTarget
+    cov = O.mvn_cov(D, rho)
+    N = 8192
+    q0 = np.random.RandomState(D).standard_normal((N, D)) @ np.linalg.cholesky(cov).T
+
+    def run():
+        h = HMC_sampler(D, None, None, Nchain=N, Niter=12, sampler_type="Random", L_low=5, L_high=20, dt=0.1,
+                        warm_up_num=2, target=MVNTarget(np.zeros(D), cov), rng="philox", seed=3, fp_mode="fast")
+        h.gen_sample(q0, verbose=False)
+        return h
+    h = run()
+    x = h.q_chain[:, 1:, :]
+    last = x[:, -1, :]                                  # one draw per chain: independent samples
+    assert np.abs(last.var(axis=0) - 1).max() < 6 * np.sqrt(2 / N)
+    assert abs(np.corrcoef(last[:, 0], last[:, 1])[0, 1] - rho) < 6 * (1 - rho ** 2) / np.sqrt(N)
+    assert 0.5 < h.accept_R <= 1.0
+    h2 = run()
+    assert np.array_equal(h.q_chain, h2.q_chain)

@@ -144,7 +144,13 @@ hmc_status hmc_chain_init(const hmc_target* t, const hmc_kinetic* k, const hmc_s
   const bool replay = s->rng_mode == HMC_RNG_REPLAY;
   if (replay && (!r || !r->p0)) return fail(HMC_EINVAL, "replay mode needs p0");
   if (s->n_chains == 0) return HMC_OK;
-  if (t->kind == HMC_TARGET_DENSE) return fail(HMC_ENOTSUP, "dense target: not in this build");
+  if (t->kind == HMC_TARGET_DENSE) {
+    if (!hmc::dense_tiles(t->D)) return fail(HMC_ENOTSUP, "dense target: D=%d > 128 not supported", t->D);
+    const hmc::Layout lay{0, 0, 0, (t->D + 1) / 2};
+    hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
+    a.qstart = q_start;
+    return hip_status(hmc::launch_dense_init(a, replay, (hipStream_t)stream), "hmc_chain_init(dense)");
+  }
   const int L_lo = s->L_high > s->L_low ? s->L_low : 5, L_hi = s->L_high > s->L_low ? s->L_high : 20;
   const hmc::Layout lay = hmc::choose_layout(t->D, L_lo, L_hi);
   if (lay.K == 0) return fail(HMC_ENOTSUP, "D=%d too large for the diagonal kernels", t->D);
@@ -163,11 +169,17 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
   const bool replay = s->rng_mode == HMC_RNG_REPLAY;
   if (replay && (!r || !r->p || !r->L || !r->lnu)) return fail(HMC_EINVAL, "replay mode needs p, L, lnu");
   if (s->n_chains == 0 || s->iter_end == s->iter_begin) return HMC_OK;
-  if (t->kind == HMC_TARGET_DENSE) return fail(HMC_ENOTSUP, "dense target: not in this build");
-  const hmc::Layout lay = hmc::choose_layout(t->D, s->L_low, s->L_high);
-  if (lay.K == 0) return fail(HMC_ENOTSUP, "D=%d too large for the diagonal kernels", t->D);
   if (st->n_save > 0 && st->traj_q && st->traj_stride < s->L_high)
     return fail(HMC_EINVAL, "traj_stride must be >= L_high");
+  if (t->kind == HMC_TARGET_DENSE) {
+    if (!hmc::dense_tiles(t->D)) return fail(HMC_ENOTSUP, "dense target: D=%d > 128 not supported", t->D);
+    const hmc::Layout lay{0, 0, 0, (t->D + 1) / 2};
+    const hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
+    return hip_status(hmc::launch_dense_iters(a, s->fp_mode == HMC_MODE_EXACT, replay, (hipStream_t)stream),
+                      "hmc_random_iters(dense)");
+  }
+  const hmc::Layout lay = hmc::choose_layout(t->D, s->L_low, s->L_high);
+  if (lay.K == 0) return fail(HMC_ENOTSUP, "D=%d too large for the diagonal kernels", t->D);
   const hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
   return hip_status(hmc::launch_random_iters(a, lay, s->fp_mode == HMC_MODE_EXACT, general_diag(t, k), replay,
                                              (hipStream_t)stream),

@@ -1,0 +1,377 @@
+// hmc_dense.hip — Random-trajectory HMC for correlated MVN targets (dense precision P = inv(cov0)).
+//
+// Replaces gen_sample_random (samplers.py:428-475) with the dense dVdq closure of the driver
+// scripts, dVdq(q) = inv_cov0 (q - q0) (case3-script.py:45-49, BASELINE config 3: D=100, rho=0.95).
+//
+// The gradient of 16 chains is one GEMM tile G^T = P . X^T on v_mfma_f64_16x16x4_f64:
+//   A = P fragment (16 dims x 4 k), read from LDS where the whole P sits as lane-linear
+//       fragments (D padded to 16*MT; MT = 7 -> 112 x 112 x 8 B = 98 KiB per block);
+//   B = X^T fragment: lane l supplies x[chain l&15][dim 4ks + (l>>4)];
+//   C = 16x16 f64 tile: lane l receives g[chain l&15][dim 16nt + (l>>4) + 4r], r < 4.
+// Lane (c = l&15, h = l>>4) therefore owns dims d = h + 4m (m < 4*MT) of chain c in BOTH the
+// accumulator and the B-operand layout: the gradient feeds the next step's B operand and the
+// elementwise kick/drift with no lane movement and no transpose (cdna_hip_programming.md §3,
+// "an accumulator tile as the next MFMA's operand").  The energy V = 0.5*(c + x.g) reuses the
+// gradient; the 4 lanes of a chain reduce with two xor-shuffles.
+// Chains of one wave can have different trajectory lengths L: the wave runs max L and
+// finished chains are masked (their gradient is recomputed at an unchanged q, bit-identical).
+#include "hmc_device.hpp"
+#include "hmc_internal.hpp"
+
+namespace hmc {
+
+namespace {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int kDenseWaves = 4;   // waves per block: one block per CU (one P copy in LDS), one wave per SIMD with the full 512-register file
+
+__device__ __forceinline__ double chain_sum4(double v) {   // sum over lanes c, c+16, c+32, c+48
+  v += __shfl_xor(v, 16, kWave);
+  v += __shfl_xor(v, 32, kWave);
+  return v;
+}
+
+template <int MT, bool GEN>
+__device__ __forceinline__ void gradient(const DenseArgs& a, const double* __restrict__ sP, int lane, int h,
+                                         const double (&q)[4 * MT], d4 (&acc)[MT]) {
+  // k-step ks: MT MFMAs (one per 16-dim output tile) with the P fragments of ks, while the
+  // fragments of ks+1 are read from LDS.  sched_barrier keeps the compiler from hoisting all
+  // 4*MT*MT fragment reads to the top (which needs hundreds of VGPRs and spills).
+  constexpr int KS = 4 * MT;
+  double af[MT], an[MT];
+#pragma unroll
+  for (int nt = 0; nt < MT; ++nt) {
+    acc[nt] = d4{0.0, 0.0, 0.0, 0.0};
+    af[nt] = sP[(nt * KS) * kWave + lane];
+  }
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (ks + 1 < KS) {
+#pragma unroll
+      for (int nt = 0; nt < MT; ++nt) an[nt] = sP[(nt * KS + ks + 1) * kWave + lane];
+    }
+    // padded dims (d >= D) meet zero columns of P, so no guard is needed here
+    const double x = (GEN && a.q0) ? q[ks] - a.q0[min(h + 4 * ks, a.D - 1)] : q[ks];
+#pragma unroll
+    for (int nt = 0; nt < MT; ++nt) acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[nt], x, acc[nt], 0, 0, 0);
+#pragma unroll
+    for (int nt = 0; nt < MT; ++nt) af[nt] = an[nt];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int MT>
+__device__ __forceinline__ double gval(const d4 (&acc)[MT], int m) {
+  return acc[m >> 2][m & 3];
+}
+
+// Per-dimension constants; the index is clamped so padded dims (whose p, q, g are all zero and
+// stay zero) never branch.
+template <int MT, bool GEN>
+__device__ __forceinline__ double dim_minv(const DenseArgs& a, int d) {
+  return (GEN && a.minv) ? a.minv[min(d, a.D - 1)] : 1.0;
+}
+
+template <int MT, bool GEN>
+__device__ __forceinline__ double dim_dt(const DenseArgs& a, int d) {
+  return (GEN && a.dtv) ? a.dtv[min(d, a.D - 1)] : a.dt;
+}
+
+template <int MT, bool EXACT, bool GEN, bool REPLAY>
+__global__ __launch_bounds__(256, 1) void k_dense_iters(DenseArgs a) {
+  constexpr int M = 4 * MT, KS = 4 * MT;
+  extern __shared__ double sP[];
+  for (int f = threadIdx.x; f < MT * KS * kWave; f += blockDim.x) {   // P fragments -> LDS (zero padded)
+    const int l = f & (kWave - 1), t = f / kWave;
+    const int nt = t / KS, ks = t - nt * KS;
+    const int n = 16 * nt + (l & 15), k = 4 * ks + (l >> 4);
+    sP[f] = (n < a.D && k < a.D) ? a.prec[(int64_t)n * a.D + k] : 0.0;
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & (kWave - 1);
+  const int h = lane >> 4;
+  const int64_t c = ((int64_t)blockIdx.x * kDenseWaves + (threadIdx.x / kWave)) * 16 + (lane & 15);
+  const bool live = c < a.n;
+  const uint64_t gc = (uint64_t)(a.chain_offset + c);
+  double q[M], p[M], qi[M];
+  d4 acc[MT];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int d = h + 4 * m;
+    q[m] = (live && d < a.D) ? a.q[c * a.D + d] : 0.0;
+  }
+  double Eprev = live ? a.Eprev[c] : 0.0;
+  unsigned long long n_acc = 0, n_acc_wu = 0, n_lf = 0, n_lf2 = 0, n_oob = 0;
+  double* const qcb = a.qc ? a.qc + c * (int64_t)a.Lc * a.D : nullptr;
+  // chain-0 trajectory capture (samplers.py:442-452): the wave holding global chain 0 (lane 0)
+  const bool cap_wave = a.traj_q && uniform_i((int)(__builtin_amdgcn_readfirstlane((int)(gc & 0xffffffff)) == 0 &&
+                                                    __builtin_amdgcn_readfirstlane((int)(gc >> 32)) == 0));
+
+  for (int it = a.it0; it < a.it1; ++it) {
+    // ---- momentum (samplers.py:431): dims h+4m; Philox pairs (m, m+1) keyed by slot h + 8*(m/2)
+    if constexpr (REPLAY) {
+      const double* row = a.rp + (c * (int64_t)a.niter + (it - 1)) * a.D;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const int d = h + 4 * m;
+        p[m] = (live && d < a.D) ? row[d] : 0.0;
+      }
+    } else {
+#pragma unroll
+      for (int m = 0; m < M; m += 2) {
+        double z0, z1;
+        normal_pair(draw_block((uint32_t)(h + 4 * m), (uint32_t)it, gc, a.k0, a.k1), z0, z1);
+        const int d0 = h + 4 * m, d1 = d0 + 4;
+        if (GEN && a.pscale) {
+          z0 *= a.pscale[min(d0, a.D - 1)];
+          z1 *= a.pscale[min(d1, a.D - 1)];
+        }
+        p[m] = d0 < a.D ? z0 : 0.0;
+        p[m + 1] = d1 < a.D ? z1 : 0.0;
+        if ((m & 6) == 6) __builtin_amdgcn_sched_barrier(0);   // bound the RNG chains in flight (registers)
+      }
+    }
+    // ---- gradient at q and E0 = V(q) + K(p)  (:434)
+    gradient<MT, GEN>(a, sP, lane, h, q, acc);
+    double maha = 0.0, kin = 0.0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {       // padded dims contribute exact zeros (g = p = 0)
+      const int d = h + 4 * m;
+      const double x = (GEN && a.q0) ? q[m] - a.q0[min(d, a.D - 1)] : q[m];
+      maha += x * gval<MT>(acc, m);
+      kin += p[m] * (dim_minv<MT, GEN>(a, d) * p[m]);
+    }
+    const double E0 = 0.5 * (a.logc + chain_sum4(maha + kin));
+    const bool post = it >= a.wu;
+    const bool write_row = post && ((it == a.niter) || ((it - a.wu + 1) % a.thin == 0));
+    const int64_t row = post ? (int64_t)((it - a.wu) / a.thin) : 0;
+    if (live && h == 0 && write_row) {
+      if (a.Ec) a.Ec[c * (int64_t)a.Lc + row] = E0;
+      if (a.dEc) a.dEc[c * (int64_t)a.Lc + row] = E0 - Eprev;
+    }
+    Eprev = E0;
+    // ---- L (:441) and log u (:461), per chain
+    int L;
+    double lnu;
+    if constexpr (REPLAY) {
+      L = live ? a.rL[c * (int64_t)a.niter + (it - 1)] : 0;
+      lnu = live ? a.rlnu[c * (int64_t)a.niter + (it - 1)] : 0.0;
+    } else {
+      const uint4 r = draw_block(kDrawSlot, (uint32_t)it, gc, a.k0, a.k1);
+      L = live ? uniform_int(r.x, a.L_low, a.L_high) : 0;
+      lnu = log(u53(r.z, r.w));
+    }
+    int Lmax = L;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) Lmax = max(Lmax, __shfl_xor(Lmax, off, kWave));
+    Lmax = uniform_i(Lmax);
+    // ---- leapfrog (:448 -> :831-839); chains with l >= L are frozen
+#pragma unroll
+    for (int m = 0; m < M; ++m) qi[m] = q[m];
+    const bool cap = cap_wave && it <= a.n_save;
+    double* capp = cap ? a.traj_q + (int64_t)(it - 1) * a.traj_stride * 2 : nullptr;
+    if (cap) {   // dims 0 and 1 of chain 0 live in lanes 0 (h=0) and 16 (h=1)
+      const double q1 = __shfl(q[0], 16, kWave);
+      if (lane == 0) {
+        capp[0] = q[0];
+        capp[1] = a.D > 1 ? q1 : q[0];
+      }
+    }
+    for (int l = 0; l < Lmax; ++l) {
+      const bool act = l < L;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const int d = h + 4 * m;
+        const double dt = dim_dt<MT, GEN>(a, d);
+        const double mi = dim_minv<MT, GEN>(a, d);
+        double ph, qn;
+        if constexpr (EXACT) {
+          ph = p[m] - (dt * (mi * gval<MT>(acc, m))) * 0.5;
+          qn = q[m] + dt * ph;
+        } else {
+          ph = __builtin_fma(-0.5 * dt * mi, gval<MT>(acc, m), p[m]);
+          qn = __builtin_fma(dt, ph, q[m]);
+        }
+        p[m] = act ? ph : p[m];
+        q[m] = act ? qn : q[m];
+        if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+      gradient<MT, GEN>(a, sP, lane, h, q, acc);
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const int d = h + 4 * m;
+        const double dt = dim_dt<MT, GEN>(a, d);
+        const double mi = dim_minv<MT, GEN>(a, d);
+        double pn;
+        if constexpr (EXACT) pn = p[m] - (dt * (mi * gval<MT>(acc, m))) * 0.5;
+        else pn = __builtin_fma(-0.5 * dt * mi, gval<MT>(acc, m), p[m]);
+        p[m] = act ? pn : p[m];
+        if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+      if (cap) {
+        const double q1 = __shfl(q[0], 16, kWave);
+        if (lane == 0 && l < L) {
+          capp[2 * (l + 1)] = q[0];
+          capp[2 * (l + 1) + 1] = a.D > 1 ? q1 : q[0];
+        }
+      }
+    }
+    // ---- E1 with the gradient of the final q, Metropolis test (:455-472)
+    maha = 0.0;
+    kin = 0.0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int d = h + 4 * m;
+      const double x = (GEN && a.q0) ? q[m] - a.q0[min(d, a.D - 1)] : q[m];
+      maha += x * gval<MT>(acc, m);
+      kin += p[m] * (dim_minv<MT, GEN>(a, d) * p[m]);
+    }
+    const double E1 = 0.5 * (a.logc + chain_sum4(maha + kin));
+    const double dE = E1 - E0;
+    const bool accept = (dE < 0.0) || (lnu < -dE);
+    if (!accept) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) q[m] = qi[m];
+    }
+    if (live && write_row && qcb) {
+      double* rowp = qcb + row * a.D;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const int d = h + 4 * m;
+        if (d < a.D) rowp[d] = q[m];
+      }
+    }
+    if (cap && lane == 0) {
+      a.traj_len[it - 1] = (L > 0 ? L : 0) + 1;
+      a.decision[it - 1] = accept ? 1 : 0;
+    }
+    if (live && h == 0) {
+      if (accept) {
+        if (post) ++n_acc; else ++n_acc_wu;
+      } else if (it < a.i_oob) {
+        ++n_oob;
+      }
+      const unsigned long long Lp = L > 0 ? (unsigned long long)L : 0ull;
+      n_lf += Lp;
+      n_lf2 += Lp * Lp;
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int d = h + 4 * m;
+    if (live && d < a.D) a.q[c * a.D + d] = q[m];
+  }
+  if (live && h == 0) a.Eprev[c] = Eprev;
+  n_acc = wave_sum_u64(n_acc);
+  n_acc_wu = wave_sum_u64(n_acc_wu);
+  n_lf = wave_sum_u64(n_lf);
+  n_lf2 = wave_sum_u64(n_lf2);
+  n_oob = wave_sum_u64(n_oob);
+  if (lane == 0 && a.cnt) {
+    const int64_t wv = (int64_t)blockIdx.x * kDenseWaves + (threadIdx.x / kWave);
+    unsigned long long* cs = a.cnt + (wv & (HMC_COUNTER_SLOTS - 1)) * HMC_NCOUNTERS;
+    if (n_acc) atomicAdd(cs + HMC_CNT_ACCEPT, n_acc);
+    if (n_acc_wu) atomicAdd(cs + HMC_CNT_ACCEPT_WU, n_acc_wu);
+    if (n_lf) atomicAdd(cs + HMC_CNT_LEAPFROG, n_lf);
+    if (n_lf2) atomicAdd(cs + HMC_CNT_LEAPFROG_SQ, n_lf2);
+    if (n_oob) atomicAdd(cs + HMC_CNT_OOB_REJECT, n_oob);
+  }
+}
+
+// Chain initialisation for dense targets (samplers.py:413-420), one thread per chain.
+template <bool REPLAY>
+__global__ __launch_bounds__(256) void k_dense_init(DenseArgs a, int MT) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.n) return;
+  const double* qs = a.qstart + c * a.D;
+  const uint64_t gc = (uint64_t)(a.chain_offset + c);
+  double maha = 0.0, kin = 0.0;
+  for (int n = 0; n < a.D; ++n) {
+    double g = 0.0;
+    for (int k = 0; k < a.D; ++k) g = __builtin_fma(a.prec[(int64_t)n * a.D + k], qs[k] - (a.q0 ? a.q0[k] : 0.0), g);
+    maha += (qs[n] - (a.q0 ? a.q0[n] : 0.0)) * g;
+  }
+  // momentum p0 with the dense kernel's Philox mapping (dims h + 4m, pair slot h + 4m, m even)
+  const int M = 4 * MT;
+  for (int h = 0; h < 4; ++h) {
+    for (int m = 0; m < M; m += 2) {
+      const int d0 = h + 4 * m, d1 = d0 + 4;
+      double z0, z1;
+      if constexpr (REPLAY) {
+        z0 = d0 < a.D ? a.rp0[c * a.D + d0] : 0.0;
+        z1 = d1 < a.D ? a.rp0[c * a.D + d1] : 0.0;
+      } else {
+        normal_pair(draw_block((uint32_t)(h + 4 * m), 0u, gc, a.k0, a.k1), z0, z1);
+        if (a.pscale) {
+          z0 = d0 < a.D ? z0 * a.pscale[d0] : 0.0;
+          z1 = d1 < a.D ? z1 * a.pscale[d1] : 0.0;
+        }
+      }
+      if (d0 < a.D) kin += z0 * ((a.minv ? a.minv[d0] : 1.0) * z0);
+      if (d1 < a.D && m + 1 < M) kin += z1 * ((a.minv ? a.minv[d1] : 1.0) * z1);
+    }
+  }
+  const double E0 = 0.5 * (a.logc + (maha + kin));
+  for (int d = 0; d < a.D; ++d) {
+    a.q[c * a.D + d] = qs[d];
+    if (a.qc) a.qc[c * (int64_t)a.Lc * a.D + d] = qs[d];
+  }
+  a.Eprev[c] = E0;
+  if (a.Ec) a.Ec[c * (int64_t)a.Lc] = E0;
+  if (a.dEc) a.dEc[c * (int64_t)a.Lc] = 0.0;
+}
+
+template <int MT, bool EXACT>
+hipError_t launch_dense_mt2(const DenseArgs& a, bool gen, bool replay, hipStream_t s) {
+  const dim3 grid((unsigned)((a.n + 16 * kDenseWaves - 1) / (16 * kDenseWaves)));
+  const size_t lds = (size_t)MT * 4 * MT * kWave * sizeof(double);
+  if (gen) {
+    if (replay) k_dense_iters<MT, EXACT, true, true><<<grid, 64 * kDenseWaves, lds, s>>>(a);
+    else k_dense_iters<MT, EXACT, true, false><<<grid, 64 * kDenseWaves, lds, s>>>(a);
+  } else {
+    if (replay) k_dense_iters<MT, EXACT, false, true><<<grid, 64 * kDenseWaves, lds, s>>>(a);
+    else k_dense_iters<MT, EXACT, false, false><<<grid, 64 * kDenseWaves, lds, s>>>(a);
+  }
+  return hipGetLastError();
+}
+
+template <int MT>
+hipError_t launch_dense_mt(const DenseArgs& a, bool exact, bool gen, bool replay, hipStream_t s) {
+  return exact ? launch_dense_mt2<MT, true>(a, gen, replay, s) : launch_dense_mt2<MT, false>(a, gen, replay, s);
+}
+
+}  // namespace
+
+int dense_tiles(int D) {
+  const int mt = (D + 15) / 16;
+  if (mt <= 1) return 1;
+  if (mt <= 2) return 2;
+  if (mt <= 4) return 4;
+  if (mt <= 7) return 7;
+  if (mt <= 8) return 8;
+  return 0;
+}
+
+hipError_t launch_dense_init(const DenseArgs& a, bool replay, hipStream_t s) {
+  const dim3 grid((unsigned)((a.n + 255) / 256));
+  const int MT = dense_tiles(a.D);
+  if (replay) k_dense_init<true><<<grid, 256, 0, s>>>(a, MT);
+  else k_dense_init<false><<<grid, 256, 0, s>>>(a, MT);
+  return hipGetLastError();
+}
+
+hipError_t launch_dense_iters(const DenseArgs& a, bool exact, bool replay, hipStream_t s) {
+  const bool gen = a.q0 || a.minv || a.pscale || a.dtv;
+  switch (dense_tiles(a.D)) {
+    case 1: return launch_dense_mt<1>(a, exact, gen, replay, s);
+    case 2: return launch_dense_mt<2>(a, exact, gen, replay, s);
+    case 4: return launch_dense_mt<4>(a, exact, gen, replay, s);
+    case 7: return launch_dense_mt<7>(a, exact, gen, replay, s);
+    case 8: return launch_dense_mt<8>(a, exact, gen, replay, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace hmc

@@ -48,30 +48,10 @@ struct RandArgs {
   unsigned long long* stamps;  // diagnostic phase timers (HMC_DEBUG_STAMPS env; null in normal runs)
 };
 
-// Dense-precision (correlated MVN) Random-trajectory kernel arguments.
-struct DenseArgs {
-  int64_t n, chain_offset;
-  int D, Dp;             // D and D padded to a multiple of 16
-  int niter, wu, thin, Lc, L_low, L_high, it0, it1, i_oob;
-  uint32_t k0, k1;
-  double dt, h, logc;
-  const double* q0;      // [D] or null
-  const double* prec;    // [D*D] row-major
-  const double* minv;    // [D] or null
-  const double* pscale;  // [D] or null
-  const double* dtv;     // [D] or null
-  const double* rp0;
-  const double* rp;
-  const double* rlnu;
-  const int32_t* rL;
-  const double* qstart;
-  double* q;
-  double* Eprev;
-  double* qc;
-  double* Ec;
-  double* dEc;
-  unsigned long long* cnt;
-};
+// Dense-precision (correlated MVN) kernels take the same argument block; `prec` is then the
+// row-major D x D precision.  dense_tiles(D) = 16-dim output tiles per chain (0: unsupported).
+using DenseArgs = RandArgs;
+int dense_tiles(int D);
 
 Layout choose_layout(int D, int L_low, int L_high);
 
