@@ -145,6 +145,23 @@ hmc_status hmc_chain_init(const hmc_target* t, const hmc_kinetic* k, const hmc_s
 hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s,
                             const hmc_replay* r /* NULL for Philox */, hmc_state* st, void* stream);
 
+/* Bytes of device workspace hmc_nuts_iters needs for n_chains chains (tree vectors: live
+ * points, both boundaries, d_max+1 save slots; replay-tape cursors).  0 if unsupported. */
+int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max);
+
+/* Iterations [iter_begin, iter_end) of the No-U-Turn sampler for all chains: momentum
+ * resample -> E0 -> tree doubling until both ends U-turn (sub-tree U-turn checks against the
+ * saved odd points, progressive sampling, biased sub-tree acceptance) -> store.
+ * Replaces HMC_sampler.gen_sample_NUTS, samplers.py:563-791 (+ utils.py:222-385).
+ * Dense precision only (pass diagonal targets as dense), D <= 128, 1 <= d_max <= 15.
+ * `workspace` (hmc_nuts_workspace_size bytes) must be zeroed before the first call of a run
+ * and kept between calls.  Counters: LEAPFROG (= ENERGY_EVALS), UNSTABLE (|E-E0| > 1000
+ * rejections, :647), DMAX (chain-iterations that reached d_max; the reference aborts there,
+ * on_dmax selects whether the caller raises), OOB_REJECT (replay tape exhausted: an error). */
+hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s,
+                          const hmc_replay* r /* NULL for Philox */, hmc_state* st, void* workspace,
+                          void* stream);
+
 /* Batched single leapfrog step (n independent (p, q) rows).
  * Replaces HMC_sampler.leap_frog(p_old, q_old), samplers.py:831-839. */
 hmc_status hmc_leapfrog(const hmc_target* t, const hmc_kinetic* k, int64_t n, const double* p,

@@ -186,6 +186,39 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
                     "hmc_random_iters");
 }
 
+int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max) {
+  if (D < 1 || n_chains < 0 || d_max < 1 || d_max > 15 || !hmc::dense_tiles(D)) return 0;
+  return hmc::nuts_ws_doubles(n_chains, D, d_max) * (int64_t)sizeof(double);
+}
+
+hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, const hmc_replay* r,
+                          hmc_state* st, void* workspace, void* stream) {
+  if (hmc_status e = check_schedule(t, k, s, false)) return e;
+  if (!st || !st->q || !st->E_prev) return fail(HMC_EINVAL, "null state");
+  if (s->iter_begin < 1 || s->iter_end < s->iter_begin || s->iter_end > s->n_iter + 1)
+    return fail(HMC_EINVAL, "iteration range must satisfy 1 <= begin <= end <= Niter+1");
+  if (s->d_max < 1 || s->d_max > 15) return fail(HMC_EINVAL, "d_max must be in [1, 15]");
+  if (t->kind != HMC_TARGET_DENSE) return fail(HMC_ENOTSUP, "NUTS runs the dense kernel: pass prec as dense");
+  if (!hmc::dense_tiles(t->D)) return fail(HMC_ENOTSUP, "dense target: D=%d > 128 not supported", t->D);
+  const bool replay = s->rng_mode == HMC_RNG_REPLAY;
+  if (replay && (!r || !r->p || !r->tape || r->tape_stride < 1)) return fail(HMC_EINVAL, "replay mode needs p and tape");
+  if (s->n_chains == 0 || s->iter_end == s->iter_begin) return HMC_OK;
+  if (!workspace) return fail(HMC_EINVAL, "null workspace");
+  const hmc::Layout lay{0, 0, 0, (t->D + 1) / 2};
+  hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
+  a.d_max = s->d_max;
+  a.on_dmax = s->on_dmax;
+  a.ws = static_cast<double*>(workspace);
+  if (replay) {
+    a.tape = r->tape;
+    a.tape_stride = r->tape_stride;
+  }
+  a.traj_q = nullptr;
+  a.n_save = 0;
+  return hip_status(hmc::launch_nuts_iters(a, s->fp_mode == HMC_MODE_EXACT, replay, (hipStream_t)stream),
+                    "hmc_nuts_iters");
+}
+
 hmc_status hmc_leapfrog(const hmc_target* t, const hmc_kinetic* k, int64_t n, const double* p, const double* q,
                         double* p_out, double* q_out, int32_t fp_mode, void* stream) {
   if (!t || !k || t->D < 1 || n < 0) return fail(HMC_EINVAL, "bad arguments");

@@ -17,78 +17,17 @@
 // finished chains are masked (their gradient is recomputed at an unchanged q, bit-identical).
 #include "hmc_device.hpp"
 #include "hmc_internal.hpp"
+#include "hmc_dense_ops.hpp"
 
 namespace hmc {
 
 namespace {
 
-typedef double d4 __attribute__((ext_vector_type(4)));
-
-constexpr int kDenseWaves = 4;   // waves per block: one block per CU (one P copy in LDS), one wave per SIMD with the full 512-register file
-
-__device__ __forceinline__ double chain_sum4(double v) {   // sum over lanes c, c+16, c+32, c+48
-  v += __shfl_xor(v, 16, kWave);
-  v += __shfl_xor(v, 32, kWave);
-  return v;
-}
-
-template <int MT, bool GEN>
-__device__ __forceinline__ void gradient(const DenseArgs& a, const double* __restrict__ sP, int lane, int h,
-                                         const double (&q)[4 * MT], d4 (&acc)[MT]) {
-  // k-step ks: MT MFMAs (one per 16-dim output tile) with the P fragments of ks, while the
-  // fragments of ks+1 are read from LDS.  sched_barrier keeps the compiler from hoisting all
-  // 4*MT*MT fragment reads to the top (which needs hundreds of VGPRs and spills).
-  constexpr int KS = 4 * MT;
-  double af[MT], an[MT];
-#pragma unroll
-  for (int nt = 0; nt < MT; ++nt) {
-    acc[nt] = d4{0.0, 0.0, 0.0, 0.0};
-    af[nt] = sP[(nt * KS) * kWave + lane];
-  }
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    if (ks + 1 < KS) {
-#pragma unroll
-      for (int nt = 0; nt < MT; ++nt) an[nt] = sP[(nt * KS + ks + 1) * kWave + lane];
-    }
-    // padded dims (d >= D) meet zero columns of P, so no guard is needed here
-    const double x = (GEN && a.q0) ? q[ks] - a.q0[min(h + 4 * ks, a.D - 1)] : q[ks];
-#pragma unroll
-    for (int nt = 0; nt < MT; ++nt) acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[nt], x, acc[nt], 0, 0, 0);
-#pragma unroll
-    for (int nt = 0; nt < MT; ++nt) af[nt] = an[nt];
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-template <int MT>
-__device__ __forceinline__ double gval(const d4 (&acc)[MT], int m) {
-  return acc[m >> 2][m & 3];
-}
-
-// Per-dimension constants; the index is clamped so padded dims (whose p, q, g are all zero and
-// stay zero) never branch.
-template <int MT, bool GEN>
-__device__ __forceinline__ double dim_minv(const DenseArgs& a, int d) {
-  return (GEN && a.minv) ? a.minv[min(d, a.D - 1)] : 1.0;
-}
-
-template <int MT, bool GEN>
-__device__ __forceinline__ double dim_dt(const DenseArgs& a, int d) {
-  return (GEN && a.dtv) ? a.dtv[min(d, a.D - 1)] : a.dt;
-}
-
 template <int MT, bool EXACT, bool GEN, bool REPLAY>
 __global__ __launch_bounds__(256, 1) void k_dense_iters(DenseArgs a) {
-  constexpr int M = 4 * MT, KS = 4 * MT;
+  constexpr int M = 4 * MT;
   extern __shared__ double sP[];
-  for (int f = threadIdx.x; f < MT * KS * kWave; f += blockDim.x) {   // P fragments -> LDS (zero padded)
-    const int l = f & (kWave - 1), t = f / kWave;
-    const int nt = t / KS, ks = t - nt * KS;
-    const int n = 16 * nt + (l & 15), k = 4 * ks + (l >> 4);
-    sP[f] = (n < a.D && k < a.D) ? a.prec[(int64_t)n * a.D + k] : 0.0;
-  }
-  __syncthreads();
+  stage_precision<MT>(a, sP);
 
   const int lane = threadIdx.x & (kWave - 1);
   const int h = lane >> 4;

@@ -43,6 +43,10 @@ struct RandArgs {
   int32_t* traj_len;
   int32_t* decision;
   int n_save, traj_stride;
+  int d_max, on_dmax;    // NUTS (hmc_nuts.hip)
+  double* ws;            // NUTS per-chain workspace (vectors: live points, boundaries, save slots)
+  const double* tape;    // NUTS replay tape [n][tape_stride] (directions / uniforms in consumption order)
+  int64_t tape_stride;
   int dbg;               // ablation flags (HMC_DEBUG_ABLATE env; 0 in normal runs)
   int dbgL;              // forced trajectory length (HMC_DEBUG_L env; -1 in normal runs)
   unsigned long long* stamps;  // diagnostic phase timers (HMC_DEBUG_STAMPS env; null in normal runs)
@@ -52,6 +56,8 @@ struct RandArgs {
 // row-major D x D precision.  dense_tiles(D) = 16-dim output tiles per chain (0: unsupported).
 using DenseArgs = RandArgs;
 int dense_tiles(int D);
+int64_t nuts_ws_doubles(int64_t n, int D, int d_max);
+hipError_t launch_nuts_iters(const RandArgs& a, bool exact, bool replay, hipStream_t s);
 
 Layout choose_layout(int D, int L_low, int L_high);
 

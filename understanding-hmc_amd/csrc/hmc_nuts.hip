@@ -1,0 +1,493 @@
+// hmc_nuts.hip — the reference's NUTS engine (samplers.py:495-808, utils.py:222-385) for many chains.
+//
+// Semantics follow gen_sample_NUTS exactly (quirks Q10-Q12 of SURVEY §8-Q): doubling until BOTH
+// ends U-turn, sub-tree U-turn checks against the saved odd points named by check_points(m)
+// with release_fast bookkeeping, progressive multinomial sampling inside the new sub-tree,
+// biased sub-tree acceptance exp(-(Emax_new-Emax_old))*pi_old/pi_new, |E - E0| > 1000 guard.
+//
+// Execution model: 16 chains per wave share the f64-MFMA gradient tile of hmc_dense_ops.hpp.
+// NUTS trees diverge per chain (7 ... 1023 leapfrogs per iteration), so each chain runs its own
+// state machine and the wave advances in *steps*: every step all chains that are inside a
+// sub-tree take exactly one leapfrog (one MFMA pass for the tile), then each chain processes its
+// new point; chains between trees (iteration end / start, sub-tree start) do their transition
+// work first.  A launch ends when every chain of the wave finished its iterations.
+// Per-chain vectors that trees keep (live points, both boundaries, the d_max+1 save slots) live
+// in a workspace in HBM (`ws`, hmc_nuts_workspace_size), stored wave-linear (vector v, element m,
+// lane) so every save/load is one fully coalesced 512-byte access and lanes never branch on the
+// dimension.  The tail of the workspace holds the per-chain replay-tape cursors (zeroed by the
+// host before the first launch of a run).  All cross-lane reductions run in converged control flow.
+#include "hmc_dense_ops.hpp"
+#include "hmc_device.hpp"
+#include "hmc_internal.hpp"
+
+namespace hmc {
+
+namespace {
+
+constexpr int kMaxDepth = 16;   // table size bound (d_max <= 15)
+
+enum : int { S_ITER_START = 0, S_SUB_START = 1, S_READY = 2, S_ITER_END = 3, S_DONE = 4 };
+
+// workspace vector ids (per chain)
+enum : int { V_OLD_Q = 0, V_OLD_G = 1, V_NEW_Q = 2, V_NEW_G = 3, V_LEFT_Q = 4, V_LEFT_P = 5, V_LEFT_G = 6,
+             V_RIGHT_Q = 7, V_RIGHT_P = 8, V_RIGHT_G = 9, V_SLOTS = 10 };
+
+__device__ __forceinline__ int nuts_nvec(int d_max) { return V_SLOTS + 2 * (d_max + 1); }
+
+// Workspace vectors are wave-linear: element m of lane l of vector v at byte
+// ((v * M + m) * 64 + l) * 8 of the wave's block, accessed through a wave-uniform buffer
+// descriptor (SGPR base, 32-bit lane offset) so no 64-bit addresses are kept live per vector.
+// `vl` is a per-lane extra vector index (the save slot of this chain), 0 for fixed vectors.
+struct WaveWS {
+  __amdgpu_buffer_rsrc_t r;
+  int lane8;
+};
+
+template <int M>
+__device__ __forceinline__ void vstore(const WaveWS& w, int v, int vl, const double (&x)[M]) {
+  const int vo = w.lane8 + vl * (M * kWave * 8);
+#pragma unroll
+  for (int m = 0; m < M; ++m)
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, x[m]), w.r,
+                                          vo, (v * M + m) * kWave * 8, 0);
+}
+
+template <int M>
+__device__ __forceinline__ double vget(const WaveWS& w, int v, int vl, int m) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(w.r, w.lane8 + vl * (M * kWave * 8),
+                                                                         (v * M + m) * kWave * 8, 0));
+}
+
+template <int M>
+__device__ __forceinline__ void vload(const WaveWS& w, int v, int vl, double (&x)[M]) {
+#pragma unroll
+  for (int m = 0; m < M; ++m) x[m] = vget<M>(w, v, vl, m);
+}
+
+template <int MT>
+__device__ __forceinline__ void gstore(const WaveWS& w, int v, int vl, const d4 (&acc)[MT]) {
+  double x[4 * MT];
+#pragma unroll
+  for (int m = 0; m < 4 * MT; ++m) x[m] = acc[m >> 2][m & 3];
+  vstore<4 * MT>(w, v, vl, x);
+}
+
+template <int MT>
+__device__ __forceinline__ void gload(const WaveWS& w, int v, int vl, d4 (&acc)[MT]) {
+#pragma unroll
+  for (int m = 0; m < 4 * MT; ++m) acc[m >> 2][m & 3] = vget<4 * MT>(w, v, vl, m);
+}
+
+// closed forms of utils.py check_points / release_fast (integer bit logic)
+__device__ __forceinline__ int cp_r(int m) {   // r of check_points(m): strip leading bits until pow2 or <= 2
+  int r = m;
+  while ((r & (r - 1)) != 0 && r > 2) r -= 1 << (31 - __builtin_clz(r));
+  return r;
+}
+__device__ __forceinline__ int cp_count(int m) {   // number of check points of even m
+  const int r = cp_r(m);
+  int cnt = 1, half = r;
+  while (half > 2) {
+    half >>= 1;
+    ++cnt;
+  }
+  return cnt;
+}
+__device__ __forceinline__ int cp_point(int m, int i) {   // i-th check point of even m
+  const int r = cp_r(m);
+  int pt = m - r + 1, half = r;
+  for (int j = 0; j < i; ++j) {
+    half >>= 1;
+    pt += half;
+  }
+  return pt;
+}
+__device__ __forceinline__ bool release_fast(int m, int l) {   // utils.py:367-385
+  int rm = m, rl = l;
+  while ((rm & (rm - 1)) != 0 && rm > 4) {
+    const int top = 1 << (31 - __builtin_clz(rm));
+    rm -= top;
+    rl -= top;
+  }
+  return (rm >= 4) && (rl > 1);
+}
+
+template <int MT, bool EXACT, bool GEN, bool REPLAY>
+__global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
+  constexpr int M = 4 * MT;
+  extern __shared__ double sP[];
+  stage_precision<MT>(a, sP);
+
+  const int lane = threadIdx.x & (kWave - 1);
+  const int h = lane >> 4;
+  const int64_t wv = (int64_t)blockIdx.x * kDenseWaves + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int64_t c = wv * 16 + (lane & 15);
+  const bool live = c < a.n;
+  const uint64_t gc = (uint64_t)(a.chain_offset + c);
+  const int64_t wave_doubles = (int64_t)nuts_nvec(a.d_max) * M * kWave;
+  const int64_t n_waves = (a.n + 15) / 16;
+  const WaveWS W{__builtin_amdgcn_make_buffer_rsrc(a.ws + wv * wave_doubles, 0, (int)(wave_doubles * 8), 0x00020000),
+                 lane * 8};
+  int64_t* const tcur = reinterpret_cast<int64_t*>(a.ws + n_waves * wave_doubles);
+
+  double q[M], p[M];
+  d4 acc[MT];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int d = h + 4 * m;
+    q[m] = (live && d < a.D) ? a.q[c * a.D + d] : 0.0;
+  }
+  double Eprev = live ? a.Eprev[c] : 0.0;
+  // gradient and potential at the starting point
+  gradient<MT, GEN>(a, sP, lane, h, q, acc);
+  double mp = 0.0;
+#pragma unroll
+  for (int m = 0; m < M; ++m) mp += ((GEN && a.q0) ? q[m] - a.q0[min(h + 4 * m, a.D - 1)] : q[m]) * gval<MT>(acc, m);
+  double maha_old = chain_sum4(mp), maha_new = 0.0;    // x.g of live_old / live_new points
+
+  int state = (live && a.it0 < a.it1) ? S_ITER_START : S_DONE;
+  int it = a.it0;
+  int d = 0, k = 0, Lsub = 1, udir = 0, ndraw = 0;
+  bool lterm = false, rterm = false;
+  double E_init = 0.0, E_max_now = 0.0, E_max_old = 0.0, pi_new = 1.0, pi_old = 1.0;
+  int table[kMaxDepth];
+#pragma unroll
+  for (int i = 0; i < kMaxDepth; ++i) table[i] = -1;
+  int64_t tpos = (REPLAY && live) ? tcur[c] : 0;        // replay tape cursor (persists across launches)
+  unsigned long long n_lf = 0, n_unst = 0, n_dmax = 0, n_tape = 0;
+
+  auto draw = [&](bool direction) -> double {           // next random number of this chain (reference order)
+    if constexpr (REPLAY) {
+      if (tpos >= a.tape_stride) {                     // exhausted tape: flagged, host raises
+        ++n_tape;
+        return direction ? 0.0 : 2.0;
+      }
+      return a.tape[c * a.tape_stride + (tpos++)];
+    } else {
+      const uint4 r = draw_block(kDrawSlot + (uint32_t)(ndraw++), (uint32_t)it, gc, a.k0, a.k1);
+      return direction ? (double)(r.x & 1u) : u53(r.z, r.w);
+    }
+  };
+  auto write_row_of = [&](int i) { return i >= a.wu && ((i == a.niter) || ((i - a.wu + 1) % a.thin == 0)); };
+
+  while (true) {
+    // ================= transitions (ITER_END -> ITER_START -> SUB_START), converged reductions
+#pragma unroll 1
+    for (int pass = 0; pass < 2; ++pass) {
+      const bool at_end = state == S_ITER_END;
+      if (at_end) {                                     // samplers.py:786-791: q = live_point_q_old
+        vload<M>(W, V_OLD_Q, 0, q);
+        gload<MT>(W, V_OLD_G, 0, acc);
+        if (write_row_of(it) && a.qc) {
+          double* rowp = a.qc + (c * (int64_t)a.Lc + (it - a.wu) / a.thin) * a.D;
+#pragma unroll
+          for (int m = 0; m < M; ++m)
+            if (h + 4 * m < a.D) rowp[h + 4 * m] = q[m];
+        }
+        Eprev = E_init;
+        ++it;
+        state = it < a.it1 ? S_ITER_START : S_DONE;
+      }
+      const bool starting = state == S_ITER_START;
+      double kin = 0.0;
+      if (starting) {                                   // momentum (:565), dims h+4m
+        if constexpr (REPLAY) {
+          const double* row = a.rp + (c * (int64_t)a.niter + (it - 1)) * a.D;
+#pragma unroll
+          for (int m = 0; m < M; ++m) p[m] = (h + 4 * m < a.D) ? row[h + 4 * m] : 0.0;
+        } else {
+#pragma unroll
+          for (int m = 0; m < M; m += 2) {
+            double z0, z1;
+            normal_pair(draw_block((uint32_t)(h + 4 * m), (uint32_t)it, gc, a.k0, a.k1), z0, z1);
+            const int d0 = h + 4 * m, d1 = d0 + 4;
+            if (GEN && a.pscale) {
+              z0 *= a.pscale[min(d0, a.D - 1)];
+              z1 *= a.pscale[min(d1, a.D - 1)];
+            }
+            p[m] = d0 < a.D ? z0 : 0.0;
+            p[m + 1] = d1 < a.D ? z1 : 0.0;
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < M; ++m) kin += p[m] * (dim_minv<MT, GEN>(a, h + 4 * m) * p[m]);
+      }
+      kin = chain_sum4(kin);
+      if (starting) {                                   // E_initial (:569), E/dE storage (:571-573)
+        E_init = 0.5 * (a.logc + (maha_old + kin));
+        if (write_row_of(it) && h == 0) {
+          const int64_t row = c * (int64_t)a.Lc + (it - a.wu) / a.thin;
+          if (a.Ec) a.Ec[row] = E_init;
+          if (a.dEc) a.dEc[row] = E_init - Eprev;
+        }
+        vstore<M>(W, V_OLD_Q, 0, q);                    // live_point_q_old = q (:577)
+        gstore<MT>(W, V_OLD_G, 0, acc);
+        double np[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) np[m] = -p[m];
+        vstore<M>(W, V_LEFT_Q, 0, q);                   // left = (q, -p), right = (q, p) (:581-584)
+        vstore<M>(W, V_LEFT_P, 0, np);
+        gstore<MT>(W, V_LEFT_G, 0, acc);
+        vstore<M>(W, V_RIGHT_Q, 0, q);
+        vstore<M>(W, V_RIGHT_P, 0, p);
+        gstore<MT>(W, V_RIGHT_G, 0, acc);
+        E_max_old = E_init;
+        pi_old = 1.0;
+        d = 0;
+        lterm = rterm = false;
+        ndraw = 0;
+        state = S_SUB_START;
+      }
+      if (state == S_SUB_START) {                       // one doubling (:595-626)
+        if (d > a.d_max - 1) {                          // :596-598 (reference aborts the run)
+          ++n_dmax;
+          state = S_ITER_END;
+        } else {
+#pragma unroll
+          for (int i = 0; i < kMaxDepth; ++i) table[i] = -1;
+          Lsub = 1 << d;
+          udir = (int)draw(true);                       // :608
+          const int b = udir == 0 ? V_RIGHT_Q : V_LEFT_Q;
+          vload<M>(W, 0, b, q);
+          vload<M>(W, 1, b, p);
+          gload<MT>(W, 2, b, acc);
+          k = 0;
+          state = S_READY;
+        }
+      }
+      // a chain that hit d_max goes round once more (ITER_END -> ITER_START -> SUB_START)
+      if (pass == 0 && !__builtin_amdgcn_ballot_w64(state == S_ITER_END)) break;
+    }
+    if (!__builtin_amdgcn_ballot_w64(state != S_DONE)) break;
+
+    // ================= one leapfrog for every chain inside a sub-tree (:612-614, :639)
+    const bool act = state == S_READY;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int dd = h + 4 * m;
+      const double dt = dim_dt<MT, GEN>(a, dd), mi = dim_minv<MT, GEN>(a, dd);
+      double ph, qn;
+      if constexpr (EXACT) {
+        ph = p[m] - (dt * (mi * gval<MT>(acc, m))) * 0.5;
+        qn = q[m] + dt * ph;
+      } else {
+        ph = __builtin_fma(-0.5 * dt * mi, gval<MT>(acc, m), p[m]);
+        qn = __builtin_fma(dt, ph, q[m]);
+      }
+      p[m] = act ? ph : p[m];
+      q[m] = act ? qn : q[m];
+      if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+    gradient<MT, GEN>(a, sP, lane, h, q, acc);
+    double mp1 = 0.0, kp1 = 0.0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int dd = h + 4 * m;
+      const double dt = dim_dt<MT, GEN>(a, dd), mi = dim_minv<MT, GEN>(a, dd);
+      double pn;
+      if constexpr (EXACT) pn = p[m] - (dt * (mi * gval<MT>(acc, m))) * 0.5;
+      else pn = __builtin_fma(-0.5 * dt * mi, gval<MT>(acc, m), p[m]);
+      p[m] = act ? pn : p[m];
+      mp1 += ((GEN && a.q0) ? q[m] - a.q0[min(dd, a.D - 1)] : q[m]) * gval<MT>(acc, m);
+      kp1 += p[m] * (mi * p[m]);
+      if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+    const double maha_pt = chain_sum4(mp1);
+    const double E_tmp = 0.5 * (a.logc + (maha_pt + chain_sum4(kp1)));   // E (:618 / :643)
+    if (act && h == 0) ++n_lf;
+
+    // ================= process the new point
+    bool reject = false, sub_end = false;
+    const int mpt = k + 1;                              // point number within the sub-tree
+    const bool first = act && k == 0, later = act && k > 0;
+    if (first) {                                        // first point (:617-626)
+      vstore<M>(W, V_NEW_Q, 0, q);
+      gstore<MT>(W, V_NEW_G, 0, acc);
+      maha_new = maha_pt;
+      E_max_now = E_tmp;
+      pi_new = 1.0;
+      table[0] = 1;
+      vstore<M>(W, V_SLOTS, 0, q);
+      vstore<M>(W, V_SLOTS + 1, 0, p);
+      k = 1;
+      sub_end = Lsub == 1;
+    } else if (later) {
+      if (fabs(E_tmp - E_init) > 1000.0) {              // :647-651
+        reject = true;
+        if (h == 0) ++n_unst;
+      } else if ((mpt & 1) == 1) {                      // odd point: save (:654-658)
+        int s = 0;
+#pragma unroll
+        for (int i = kMaxDepth - 1; i >= 0; --i)
+          if (table[i] == -1 && i <= a.d_max) s = i;      // find_next
+#pragma unroll
+        for (int i = 0; i < kMaxDepth; ++i)
+          if (i == s) table[i] = mpt;
+        vstore<M>(W, V_SLOTS, 2 * s, q);
+        vstore<M>(W, V_SLOTS + 1, 2 * s, p);
+      }
+    }
+    // even point: sub-tree U-turn checks against check_points(mpt) (:699-736), converged loop
+    const bool checking = later && !reject && (mpt & 1) == 0;
+    const int ncheck = checking ? cp_count(mpt) : 0;
+    int ncheck_w = ncheck;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) ncheck_w = max(ncheck_w, __shfl_xor(ncheck_w, off, kWave));
+    ncheck_w = uniform_i(ncheck_w);
+    bool alive_chk = checking;
+    for (int ci = 0; ci < ncheck_w; ++ci) {
+      const bool doit = alive_chk && ci < ncheck;
+      const int l = doit ? cp_point(mpt, ci) : 0;
+      int s = 0;
+#pragma unroll
+      for (int i = 0; i < kMaxDepth; ++i)
+        if (table[i] == l) s = i;                       // retrieve_save_index (unique match)
+      double r_dot = 0.0, l_dot = 0.0;
+      if (doit) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          // forward: left = (q_check, -p_check), right = (q, p); backward: left = (q, p), right = (q_check, -p_check)
+          const double qc = vget<M>(W, V_SLOTS, 2 * s, m), pc = vget<M>(W, V_SLOTS + 1, 2 * s, m);
+          const double Dq = udir == 0 ? q[m] - qc : qc - q[m];
+          const double rp = udir == 0 ? p[m] : -pc;
+          const double lp = udir == 0 ? -pc : p[m];
+          r_dot += Dq * rp;
+          l_dot += -Dq * lp;
+          if ((m & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      r_dot = chain_sum4(r_dot);
+      l_dot = chain_sum4(l_dot);
+      if (doit) {
+        if (l_dot < 0.0 && r_dot < 0.0) {               // :727-732
+          reject = true;
+          alive_chk = false;
+        } else if (l > 1 && release_fast(mpt, l)) {     // :735-736
+#pragma unroll
+          for (int i = 0; i < kMaxDepth; ++i)
+            if (i == s) table[i] = -1;
+        }
+      }
+    }
+    if (later && !reject) {                             // progressive sampling (:743-751)
+      const double E_max_prev = E_max_now;
+      E_max_now = fmax(E_max_prev, E_tmp);
+      const double num = exp(-(E_tmp - E_max_now));
+      pi_new = num + exp(E_max_now - E_max_prev) * pi_new;
+      const double r = num / pi_new;
+      if (draw(false) < r) {
+        vstore<M>(W, V_NEW_Q, 0, q);
+        gstore<MT>(W, V_NEW_G, 0, acc);
+        maha_new = maha_pt;
+      }
+      ++k;
+      sub_end = k == Lsub;
+    }
+    if (act && reject) state = S_ITER_END;               // q = live_point_q_old (:649, :731)
+
+    // ================= sub-tree end: boundary, biased acceptance, termination (:757-784)
+    double tr = 0.0, tl = 0.0;
+    if (sub_end) {
+      const int b = udir == 0 ? V_RIGHT_Q : V_LEFT_Q;    // this end <- (q, p)
+      vstore<M>(W, 0, b, q);
+      vstore<M>(W, 1, b, p);
+      gstore<MT>(W, 2, b, acc);
+      const double r = exp(-(E_max_now - E_max_old)) * pi_old / pi_new;   // :766 (Q11)
+      const double E_max_old_prev = E_max_old;
+      E_max_old = fmax(E_max_old_prev, E_max_now);
+      pi_old = exp(-(E_max_now - E_max_old)) * pi_new + exp(-(E_max_old_prev - E_max_old)) * pi_old;
+      const double A = fmin(1.0, r);
+      if (draw(false) < A) {                            // :773-775
+        double t[M];
+        vload<M>(W, V_NEW_Q, 0, t);
+        vstore<M>(W, V_OLD_Q, 0, t);
+        vload<M>(W, V_NEW_G, 0, t);
+        vstore<M>(W, V_OLD_G, 0, t);
+        maha_old = maha_new;
+      }
+      const int o = udir == 0 ? V_LEFT_Q : V_RIGHT_Q;   // the other end
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const double oq = vget<M>(W, 0, o, m), op = vget<M>(W, 1, o, m);
+        if ((m & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+        const double rq = udir == 0 ? q[m] : oq, lq = udir == 0 ? oq : q[m];
+        const double rpp = udir == 0 ? p[m] : op, lpp = udir == 0 ? op : p[m];
+        const double Dq = rq - lq;
+        tr += Dq * rpp;
+        tl += -Dq * lpp;
+      }
+    }
+    tr = chain_sum4(tr);
+    tl = chain_sum4(tl);
+    if (sub_end) {                                      // :779-784 (Q10: stop when BOTH ends turn)
+      rterm = tr < 0.0;
+      lterm = tl < 0.0;
+      ++d;
+      state = (lterm && rterm) ? S_ITER_END : S_SUB_START;
+    }
+  }
+
+  // write back chain state and counters
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int dd = h + 4 * m;
+    if (live && dd < a.D) a.q[c * a.D + dd] = q[m];
+  }
+  if (live && h == 0) a.Eprev[c] = Eprev;
+  if (REPLAY && live && h == 0) tcur[c] = tpos;
+  n_lf = wave_sum_u64(n_lf);
+  n_unst = wave_sum_u64(n_unst);
+  n_dmax = wave_sum_u64(live && h == 0 ? n_dmax : 0ull);
+  n_tape = wave_sum_u64(live && h == 0 ? n_tape : 0ull);
+  if (lane == 0 && a.cnt) {
+    unsigned long long* cs = a.cnt + (wv & (HMC_COUNTER_SLOTS - 1)) * HMC_NCOUNTERS;
+    if (n_lf) {
+      atomicAdd(cs + HMC_CNT_LEAPFROG, n_lf);
+      atomicAdd(cs + HMC_CNT_ENERGY_EVALS, n_lf);
+    }
+    if (n_unst) atomicAdd(cs + HMC_CNT_UNSTABLE, n_unst);
+    if (n_dmax) atomicAdd(cs + HMC_CNT_DMAX, n_dmax);
+    if (n_tape) atomicAdd(cs + HMC_CNT_OOB_REJECT, n_tape);   // NUTS: replay tape exhausted
+  }
+}
+
+template <int MT, bool EXACT>
+hipError_t launch_nuts_mt2(const RandArgs& a, bool gen, bool replay, hipStream_t s) {
+  const dim3 grid((unsigned)((a.n + 16 * kDenseWaves - 1) / (16 * kDenseWaves)));
+  const size_t lds = (size_t)MT * 4 * MT * kWave * sizeof(double);
+  if (gen) {
+    if (replay) k_nuts_iters<MT, EXACT, true, true><<<grid, 64 * kDenseWaves, lds, s>>>(a);
+    else k_nuts_iters<MT, EXACT, true, false><<<grid, 64 * kDenseWaves, lds, s>>>(a);
+  } else {
+    if (replay) k_nuts_iters<MT, EXACT, false, true><<<grid, 64 * kDenseWaves, lds, s>>>(a);
+    else k_nuts_iters<MT, EXACT, false, false><<<grid, 64 * kDenseWaves, lds, s>>>(a);
+  }
+  return hipGetLastError();
+}
+
+template <int MT>
+hipError_t launch_nuts_mt(const RandArgs& a, bool exact, bool gen, bool replay, hipStream_t s) {
+  return exact ? launch_nuts_mt2<MT, true>(a, gen, replay, s) : launch_nuts_mt2<MT, false>(a, gen, replay, s);
+}
+
+}  // namespace
+
+int64_t nuts_ws_doubles(int64_t n, int D, int d_max) {
+  const int MT = dense_tiles(D);
+  const int64_t waves = (n + 15) / 16;
+  return waves * (int64_t)(V_SLOTS + 2 * (d_max + 1)) * 4 * MT * kWave + waves * 16;   // vectors + tape cursors
+}
+
+hipError_t launch_nuts_iters(const RandArgs& a, bool exact, bool replay, hipStream_t s) {
+  const bool gen = a.q0 || a.minv || a.pscale || a.dtv;
+  switch (dense_tiles(a.D)) {
+    case 1: return launch_nuts_mt<1>(a, exact, gen, replay, s);
+    case 2: return launch_nuts_mt<2>(a, exact, gen, replay, s);
+    case 4: return launch_nuts_mt<4>(a, exact, gen, replay, s);
+    case 7: return launch_nuts_mt<7>(a, exact, gen, replay, s);
+    case 8: return launch_nuts_mt<8>(a, exact, gen, replay, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace hmc

@@ -19,7 +19,7 @@ def _dev(a, device, dtype=torch.float64):
 class RandomEngine:
     def __init__(self, target, n_chains, n_iter, warm_up, thin, L_low, L_high, dt, cov_p=None, rng="philox",
                  seed=0, fp_mode="fast", chain_offset=0, store_chain=True, store_energy=True, n_save=0,
-                 device=None):
+                 device=None, dense=False):
         self.t = target
         self.D = D = target.D
         self.N = int(n_chains)
@@ -31,9 +31,10 @@ class RandomEngine:
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         dev = self.device
         # ---- target / kinetic descriptors (kept alive on the object)
-        kind = H.HMC_TARGET_DIAG if target.diagonal else H.HMC_TARGET_DENSE
+        diag = target.diagonal and not dense
+        kind = H.HMC_TARGET_DIAG if diag else H.HMC_TARGET_DENSE
         self._q0 = None if target.zero_mean else _dev(target.q0, dev)
-        if target.diagonal:
+        if diag:
             self._prec = None if target.identity else _dev(np.diag(target.prec), dev)
         else:
             self._prec = _dev(target.prec, dev)
@@ -81,11 +82,14 @@ class RandomEngine:
         self._streams = [_dev(p0, dev), _dev(P, dev), _dev(Ls, dev, torch.int32), _dev(lnu, dev)]
         self._replay = H.Replay(*[H.ptr(x) for x in self._streams], None, 0)
 
+    d_max, on_dmax = 10, 0
+
     def schedule(self, it0, it1):
         return H.Schedule(self.N, self.chain_offset, self.n_iter, self.warm_up, self.thin, self.L_chain,
                           self.L_low, self.L_high, it0, it1,
                           H.HMC_RNG_REPLAY if self.rng == "replay" else H.HMC_RNG_PHILOX,
-                          H.HMC_MODE_EXACT if self.fp_mode == "exact" else H.HMC_MODE_FAST, 10, 0, self.seed)
+                          H.HMC_MODE_EXACT if self.fp_mode == "exact" else H.HMC_MODE_FAST, self.d_max,
+                          self.on_dmax, self.seed)
 
     def stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -104,3 +108,37 @@ class RandomEngine:
 
     def read_counters(self):
         return self.counters.cpu().numpy().astype(np.int64).sum(axis=0)
+
+
+class NutsEngine(RandomEngine):
+    """Chain batch of the No-U-Turn sampler (samplers.py:495-808) on the dense-precision
+    MFMA kernel (hmc_nuts_iters).  Diagonal targets are passed as dense precisions.
+    `run(it0, it1)` advances every chain through iterations [it0, it1) in one launch; the
+    tree workspace (live points, both ends, d_max+1 save slots per chain) stays on the device."""
+
+    def __init__(self, target, n_chains, n_iter, warm_up, thin, d_max, dt, cov_p=None, rng="philox", seed=0,
+                 fp_mode="fast", chain_offset=0, store_chain=True, store_energy=True, on_dmax="raise",
+                 device=None):
+        super().__init__(target, n_chains, n_iter, warm_up, thin, 5, 20, dt, cov_p=cov_p, rng=rng, seed=seed,
+                         fp_mode=fp_mode, chain_offset=chain_offset, store_chain=store_chain,
+                         store_energy=store_energy, n_save=0, device=device, dense=True)
+        assert on_dmax in ("raise", "break")
+        self.d_max = int(d_max)
+        self.on_dmax = 0 if on_dmax == "raise" else 1
+        nbytes = H.lib().hmc_nuts_workspace_size(self.D, self.N, self.d_max)
+        if nbytes <= 0:
+            raise NotImplementedError("NUTS kernel: D=%d / d_max=%d not supported (D <= 128, 1 <= d_max <= 15)"
+                                      % (self.D, self.d_max))
+        self.ws = torch.zeros((nbytes + 7) // 8, dtype=torch.float64, device=self.device)
+
+    def set_replay(self, p0, P, tape):
+        """Host-replayed draws: p0 (N,D), p (N,Niter,D), tape (N,T) directions/uniforms in order."""
+        dev = self.device
+        tape = np.ascontiguousarray(tape, dtype=np.float64)
+        self._streams = [_dev(p0, dev), _dev(P, dev), _dev(tape, dev)]
+        self._replay = H.Replay(H.ptr(self._streams[0]), H.ptr(self._streams[1]), None, None,
+                                H.ptr(self._streams[2]), tape.shape[1])
+
+    def run(self, it0, it1):
+        H.check(H.lib().hmc_nuts_iters(self.T, self.K, self.schedule(it0, it1), self._replay, self.S,
+                                       H.ptr(self.ws), self.stream()), "hmc_nuts_iters")

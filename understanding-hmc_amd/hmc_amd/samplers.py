@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from . import _lib as H
-from .engine import RandomEngine
+from .engine import NutsEngine, RandomEngine
 from .target import MVNTarget, probe_closures  # noqa: F401
 from . import utils as U
 
@@ -255,8 +255,69 @@ class HMC_sampler(sampler):
             tl = eng.traj_len.cpu().numpy()
             self.phi_q = [T_[i, :tl[i]].copy() for i in range(n_save) if tl[i] > 0]
 
-    def gen_sample_NUTS(self, q_start, N_save_chain0, verbose):
-        raise NotImplementedError("NUTS kernel not in this build yet")
+    def set_nuts_replay(self, p0, P, tape):
+        """Explicit NUTS draw streams (rng="replay"): p0 (Nchain, D), p (Nchain, Niter, D) and a
+        per-chain tape (Nchain, T) of the directions (:608) and uniforms (:750, :773) in the
+        order the reference consumes them.  NUTS interleaves these draws with the data-dependent
+        tree, so they cannot be pre-drawn from the global np.random; without a tape,
+        rng="replay" NUTS runs the Philox streams keyed by a seed drawn from np.random (so
+        np.random.seed still makes the run reproducible)."""
+        self._nuts_replay = (np.asarray(p0, np.float64), np.asarray(P, np.float64), np.asarray(tape, np.float64))
+
+    def gen_sample_NUTS(self, q_start, N_save_chain0, verbose, on_dmax="raise"):
+        """samplers.py:495-808 on the GPU (hmc_nuts_iters via NutsEngine).  The reference's
+        `assert False` at d > d_max-1 (:596-598) becomes AssertionError after the run
+        (on_dmax="raise") or keeps the current sample (on_dmax="break")."""
+        q_start = np.asarray(q_start, dtype=np.float64)
+        assert q_start.shape[0] == self.Nchain                                    # :510
+        if N_save_chain0 > 0:
+            self.phi_q = []                                                       # :511-514 (never filled)
+        torch.cuda.set_device(self.device)
+        tape = getattr(self, "_nuts_replay", None)
+        rng, seed = self.rng, self.seed
+        if rng == "replay" and tape is None:
+            rng, seed = "philox", int(np.random.randint(0, 2 ** 62, dtype=np.int64))
+        eng = NutsEngine(self.target(), self.Nchain, self.Niter, self.warm_up_num, self.thin_rate, self.d_max,
+                         self.dt, cov_p=self.cov_p, rng=rng, seed=seed, fp_mode=self.fp_mode,
+                         chain_offset=self.chain_offset, store_chain=self.store_chain, on_dmax=on_dmax,
+                         device=self.device)
+        if rng == "replay":
+            eng.set_replay(*tape)
+        t0 = time.time()
+        eng.init(q_start.reshape(self.Nchain, self.D))
+        step = self.iters_per_launch or self.Niter
+        for it0 in range(1, self.Niter + 1, step):
+            eng.run(it0, min(it0 + step, self.Niter + 1))
+        torch.cuda.synchronize(self.device)
+        elapsed = time.time() - t0
+        c = eng.read_counters()
+        if c[H.CNT_OOB_REJECT] > 0:
+            raise IndexError("NUTS replay tape exhausted")
+        if c[H.CNT_DMAX] > 0 and on_dmax == "raise":
+            raise AssertionError("Doubling number d exceeds d_max = %d" % self.d_max)   # :596-598
+        N, D = self.Nchain, self.D
+        self.n_leapfrog = int(c[H.CNT_LEAPFROG])
+        self.n_unstable = int(c[H.CNT_UNSTABLE])
+        self.n_dmax = int(c[H.CNT_DMAX])
+        self.N_total_steps += N * (1 + self.Niter) + (D + 1) * self.n_leapfrog  # :553, :570, :614-619, :640-644
+        if verbose:
+            self.dt_total += elapsed
+            print("Ran %d NUTS chains on %s: %.2f s" % (N, self.device, elapsed))
+        self.engine = eng
+        self.q_chain_device = eng.q_chain
+        self.q_device = eng.q
+        if eng.q_chain is not None:
+            self.q_chain = eng.q_chain.cpu().numpy()
+        self.E_chain = eng.E_chain.cpu().numpy()[:, :, None]
+        self.dE_chain = eng.dE_chain.cpu().numpy()[:, :, None]
+        print("Compute acceptance rate: By default equal to 1.")                 # :800-805
+        if self.warm_up_num > 0:
+            self.accept_R_warm_up = 1.
+            print("During warm up: %.3f" % self.accept_R_warm_up)
+        self.accept_R = 1.
+        print("After warm up: %.3f" % self.accept_R)
+        print("Completed.")
+        return
 
     # ------------------------------------------------------------------ primitives (batched on GPU)
     def leap_frog(self, p_old, q_old):
