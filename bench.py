@@ -40,6 +40,9 @@ def parse():
     ap.add_argument("--dt", type=float, default=0.1)
     ap.add_argument("--rho", type=float, default=0.0, help="MVN correlation (0: unit/diagonal kernel; "
                     ">0: dense precision, MFMA kernel, BASELINE config 3 uses 0.95 with 262144 chains)")
+    ap.add_argument("--sampler", default="random", choices=["random", "nuts"],
+                    help="nuts: BASELINE config 5 (use with --rho 0.95 --chains 65536 --iters-per-step 2)")
+    ap.add_argument("--d-max", type=int, default=10)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget per process")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ess", action="store_true")
@@ -48,24 +51,28 @@ def parse():
 
 # ------------------------------------------------------------------ CPU baseline (oracle port)
 def _cpu_worker(args):
-    seed, D, budget = args
+    seed, D, budget, rho, sampler, d_max = args
     os.environ["OMP_NUM_THREADS"] = "1"
     from oracle import hmc_oracle as O
     np.random.seed(seed)
-    tgt = O.MVNTarget(np.zeros(D), np.eye(D))
+    cov = np.eye(D) if rho == 0 else O.mvn_cov(D, rho)
+    tgt = O.MVNTarget(np.zeros(D), cov)
     core = O.HMCCore(tgt, 0.1)
     q_start = O.start_pts(np.zeros(D), 2 * np.eye(D), 1)
     lf = 0
     t0 = time.time()
-    # rounds of 20 iterations of the reference-equivalent engine until the budget is spent
+    # rounds of iterations of the reference-equivalent engine until the budget is spent
     while time.time() - t0 < budget:
-        out = O.gen_sample_random(core, q_start, 1, 20, 0, 1, 5, 20, O.LiveDraws(D, np.eye(D)))
+        if sampler == "nuts":
+            out = O.gen_sample_nuts(core, q_start, 1, 2, 0, 1, d_max, O.LiveDraws(D, np.eye(D)), on_dmax="break")
+        else:
+            out = O.gen_sample_random(core, q_start, 1, 20, 0, 1, 5, 20, O.LiveDraws(D, np.eye(D)))
         lf += out["n_leapfrog"]
         q_start = out["q_chain"][:, -1, :]
     return lf, time.time() - t0
 
 
-def cpu_baseline(D, budget):
+def cpu_baseline(D, budget, rho=0.0, sampler="random", d_max=10):
     try:
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
@@ -76,7 +83,7 @@ def cpu_baseline(D, budget):
         os.environ[k] = "1"
     ctx = mp.get_context("spawn")
     with ctx.Pool(procs) as pool:
-        res = pool.map(_cpu_worker, [(1000 + i, D, budget) for i in range(procs)])
+        res = pool.map(_cpu_worker, [(1000 + i, D, budget, rho, sampler, d_max) for i in range(procs)])
     for k, v in env_threads.items():
         if v is None:
             os.environ.pop(k, None)
@@ -85,8 +92,8 @@ def cpu_baseline(D, budget):
     lf = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
     return dict(value=lf / wall, unit="leapfrog steps/s", cores=procs, kind="port",
-                sample=f"oracle/hmc_oracle.py Random engine (reference-equivalent NumPy: eigh logpdf per E, "
-                       f"SVD mvn per draw), D={D} unit MVN, {procs} procs x 1 chain x ~{budget:.0f} s, "
+                sample=f"oracle/hmc_oracle.py {sampler} engine (reference-equivalent NumPy: eigh logpdf per E, "
+                       f"SVD mvn per draw), D={D} rho={rho}, {procs} procs x 1 chain x ~{budget:.0f} s, "
                        f"{lf} leapfrogs")
 
 
@@ -114,7 +121,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from hmc_amd.engine import RandomEngine
+    from hmc_amd.engine import NutsEngine, RandomEngine
     from hmc_amd.target import MVNTarget
     from hmc_amd import _lib as H
     from hmc_amd.diagnostics import convergence_stats
@@ -125,8 +132,13 @@ def main():
     wu = W * S + 1                     # q_chain rows 0..K*S hold exactly the timed iterations
     cov = np.eye(D) if a.rho == 0 else (np.diag(np.ones(D)) * (1 - a.rho) + a.rho)
     tgt = MVNTarget(np.zeros(D), cov)
-    eng = RandomEngine(tgt, N, n_iter, wu, 1, 5, 20, a.dt, rng="philox", seed=a.seed, fp_mode=a.fp_mode,
-                       chain_offset=rank * N, store_chain=not a.no_ess, device=dev)
+    nuts = a.sampler == "nuts"
+    if nuts:
+        eng = NutsEngine(tgt, N, n_iter, wu, 1, a.d_max, a.dt, rng="philox", seed=a.seed, fp_mode=a.fp_mode,
+                         chain_offset=rank * N, store_chain=not a.no_ess, on_dmax="break", device=dev)
+    else:
+        eng = RandomEngine(tgt, N, n_iter, wu, 1, 5, 20, a.dt, rng="philox", seed=a.seed, fp_mode=a.fp_mode,
+                           chain_offset=rank * N, store_chain=not a.no_ess, device=dev)
     rs = np.random.RandomState(a.seed + rank)
     eng.init(torch.as_tensor(rs.standard_normal((N, D)) * np.sqrt(2.0), device=dev))
     it = 1
@@ -155,6 +167,7 @@ def main():
     c1 = eng.read_counters()
     lf_local = int(c1[H.CNT_LEAPFROG] - c0[H.CNT_LEAPFROG])
     acc = int(c1[H.CNT_ACCEPT] - c0[H.CNT_ACCEPT])
+    wave_steps = int(c1[H.CNT_LEAPFROG_SQ] - c0[H.CNT_LEAPFROG_SQ])   # NUTS: steps of 16-chain waves
     tot = torch.tensor([float(lf_local), float(acc), elapsed, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
         s = tot[:2].clone()
@@ -178,14 +191,26 @@ def main():
         row_bytes = 8 * D if eng.q_chain is not None else 0
         bytes_launch = N * (S * (row_bytes + 16) + 16 * D + 16)
         lf_launch = lf_local / K
-        # algorithmic flops: 8D per leapfrog + 8D energies per iteration
-        flops_launch = lf_launch * 8 * D + N * S * 8 * D
+        dense = a.rho != 0 or nuts
+        if dense:   # 2D^2 + 7D per leapfrog (Random dense), 2D^2 + 12D (NUTS: E + U-turn dots)
+            flops_launch = lf_launch * (2 * D * D + (12 if nuts else 7) * D)
+        else:       # 8D per leapfrog + 8D energies per iteration
+            flops_launch = lf_launch * 8 * D + N * S * 8 * D
         kern_s = kern_ms / 1e3
         gbs = bytes_launch / kern_s / 1e9
         tfl = flops_launch / kern_s / 1e12
-        traffic = pmc_traffic()
+        traffic = pmc_traffic() if not dense and not nuts else None
+        kname = "hmc_nuts_iters" if nuts else ("hmc_random_iters(dense)" if dense else "hmc_random_iters")
+        hbm = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+               "traffic": None if traffic is None else traffic.get("bytes_per_launch"),
+               "kernel": kname, "kernel_ms": kern_ms, "bytes_per_launch": bytes_launch}
+        mfma = {"bound": "mfma" if dense else "fp64 vector", "achieved": tfl, "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": tfl / FP64_PEAK_TFLOPS, "traffic": None, "kernel": kname,
+                "kernel_ms": kern_ms, "flops_per_launch": flops_launch}
+        tdesc = f"rho={a.rho} dense-precision MVN" if a.rho != 0 else "unit MVN"
+        samp = f"NUTS d_max={a.d_max} (overflow counted, not aborted)" if nuts else "Random-L HMC, L~U{5..19}"
         line = {
-            "metric": "leapfrog steps/sec (whole node) + ESS/sec, D=100 MVN",
+            "metric": "leapfrog steps/sec (whole node) + ESS/sec, D=100 MVN at 1M chains",
             "value": value,
             "unit": "leapfrog steps/s",
             "n_gpus": world,
@@ -196,23 +221,20 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (D=100 unit MVN, starts ~ N(0, 2I), Philox4x32-10 draws)",
-            "config": {"workload": f"Random-L HMC, D={D} unit MVN, dt=0.1, L~U{{5..19}}, {N} chains/GPU "
+            "data": f"synthetic (D={D} {tdesc}, starts ~ N(0, 2I), Philox4x32-10 draws)",
+            "config": {"workload": f"{samp}, D={D} {tdesc}, dt={a.dt}, {N} chains/GPU "
                                    f"({N * world} total), {S} iterations per step (one fused launch), "
                                    f"fp_mode={a.fp_mode}",
                        "chains_per_gpu": N, "dim": D, "iters_per_step": S, "parallelism": f"chains{world}"},
-            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": gbs / HBM_PEAK_GBS,
-                         "traffic": None if traffic is None else traffic.get("bytes_per_launch"),
-                         "kernel": "hmc_random_iters", "kernel_ms": kern_ms,
-                         "bytes_per_launch": bytes_launch},
-            "compute": {"bound": "fp64 vector", "achieved": tfl, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                        "frac": tfl / FP64_PEAK_TFLOPS, "flops_per_launch": flops_launch},
-            "accept_rate": acc_all / (N * world * K * S),
+            "roofline": mfma if dense else hbm,
+            "compute" if not dense else "memory": mfma if not dense else hbm,
+            "accept_rate": None if nuts else acc_all / (N * world * K * S),
+            "leapfrog_per_iteration": lf_all / (N * world * K * S),
+            "lane_utilisation": (lf_local / (16.0 * wave_steps)) if nuts and wave_steps else None,
             "ess": ess,
         }
         if world == 1 and not a.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(D, a.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(D, a.cpu_seconds, a.rho, a.sampler, a.d_max)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

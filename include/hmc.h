@@ -47,7 +47,7 @@ enum {
   HMC_CNT_ACCEPT = 0,        /* accepted proposals, i >= warm_up (samplers.py:467)          */
   HMC_CNT_ACCEPT_WU = 1,     /* accepted proposals, i <  warm_up (samplers.py:469)          */
   HMC_CNT_LEAPFROG = 2,      /* sum of L actually integrated (the metric's unit of work)     */
-  HMC_CNT_LEAPFROG_SQ = 3,   /* sum of L^2 (reproduces N_total_steps, Q13)                   */
+  HMC_CNT_LEAPFROG_SQ = 3,   /* Random: sum of L^2 (N_total_steps, Q13); NUTS: wave steps    */
   HMC_CNT_OOB_REJECT = 4,    /* rejections whose warm-up row index is < -L_chain (Q5)        */
   HMC_CNT_UNSTABLE = 5,      /* NUTS |E-E0| > 1000 sub-tree rejections (samplers.py:647)     */
   HMC_CNT_DMAX = 6,          /* NUTS chain-iterations that hit d_max                         */

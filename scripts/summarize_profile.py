@@ -11,6 +11,7 @@ import shutil
 import sys
 
 out, tag = sys.argv[1], sys.argv[2]
+write_traffic_file = "--no-traffic-file" not in sys.argv[3:]
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(ROOT, "profiles")
 os.makedirs(prof, exist_ok=True)
@@ -56,16 +57,18 @@ if fetch_kb is not None and write_kb is not None:
     summary["write_size_kb"] = write_kb
     summary["bytes_per_launch"] = (2.0 * fetch_kb + write_kb) * 1024.0
 sq = {}
-f = one("sq/**/run_counter_collection.csv")
-if f:
-    agg = {}
-    for r in csv.DictReader(open(f)):
-        if any(h in r["Kernel_Name"] for h in HOT):
-            agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-    sq = {k: sum(v) / len(v) for k, v in agg.items()}
+for sub in ("sq", "sq2"):
+    f = one(f"{sub}/**/run_counter_collection.csv")
+    if f:
+        agg = {}
+        for r in csv.DictReader(open(f)):
+            if any(h in r["Kernel_Name"] for h in HOT):
+                agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+        sq.update({k: sum(v) / len(v) for k, v in agg.items()})
+if sq:
     summary["sq"] = sq
 json.dump(summary, open(os.path.join(prof, f"{tag}_profile_summary.json"), "w"), indent=1)
-if "bytes_per_launch" in summary:
+if "bytes_per_launch" in summary and write_traffic_file:
     json.dump({"bytes_per_launch": summary["bytes_per_launch"], "source": f"profiles/{tag}_profile_summary.json",
                "kernel": summary.get("hot_kernel")},
               open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)

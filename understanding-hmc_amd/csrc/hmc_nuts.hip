@@ -12,9 +12,8 @@
 // new point; chains between trees (iteration end / start, sub-tree start) do their transition
 // work first.  A launch ends when every chain of the wave finished its iterations.
 // Per-chain vectors that trees keep (live points, both boundaries, the d_max+1 save slots) live
-// in a workspace in HBM (`ws`, hmc_nuts_workspace_size), stored wave-linear (vector v, element m,
-// lane) so every save/load is one fully coalesced 512-byte access and lanes never branch on the
-// dimension.  The tail of the workspace holds the per-chain replay-tape cursors (zeroed by the
+// in a workspace in HBM (`ws`, hmc_nuts_workspace_size), chain-contiguous and zero padded so
+// lanes never branch on the dimension and chains that sit out a branch move no bytes.  The tail of the workspace holds the per-chain replay-tape cursors (zeroed by the
 // host before the first launch of a run).  All cross-lane reductions run in converged control flow.
 #include "hmc_dense_ops.hpp"
 #include "hmc_device.hpp"
@@ -34,28 +33,36 @@ enum : int { V_OLD_Q = 0, V_OLD_G = 1, V_NEW_Q = 2, V_NEW_G = 3, V_LEFT_Q = 4, V
 
 __device__ __forceinline__ int nuts_nvec(int d_max) { return V_SLOTS + 2 * (d_max + 1); }
 
-// Workspace vectors are wave-linear: element m of lane l of vector v at byte
-// ((v * M + m) * 64 + l) * 8 of the wave's block, accessed through a wave-uniform buffer
-// descriptor (SGPR base, 32-bit lane offset) so no 64-bit addresses are kept live per vector.
+// Workspace: per chain, nvec vectors of Dp = 4M doubles (dims, zero padded), chain-contiguous,
+// 16 chains of a wave in one block addressed through a wave-uniform buffer descriptor (SGPR base,
+// 32-bit lane offset: no 64-bit addresses kept live).  Lane (c, h) touches dims h + 4m, so one
+// chain's part of an access is 32 contiguous bytes: lanes of chains that sit out a branch cost
+// no memory traffic (a wave-linear layout would fetch whole lines for every masked access).
 // `vl` is a per-lane extra vector index (the save slot of this chain), 0 for fixed vectors.
 struct WaveWS {
   __amdgpu_buffer_rsrc_t r;
-  int lane8;
+  int lane_off;   // (lane & 15) * nvec * Dp * 8 + h * 8
 };
 
 template <int M>
 __device__ __forceinline__ void vstore(const WaveWS& w, int v, int vl, const double (&x)[M]) {
-  const int vo = w.lane8 + vl * (M * kWave * 8);
+  const int vo = w.lane_off + vl * (4 * M * 8);
 #pragma unroll
   for (int m = 0; m < M; ++m)
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, x[m]), w.r,
-                                          vo, (v * M + m) * kWave * 8, 0);
+                                          vo, v * (4 * M * 8) + m * 32, 0);
+}
+
+template <int M>
+__device__ __forceinline__ void vput(const WaveWS& w, int v, int m, double x) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, x), w.r,
+                                        w.lane_off, v * (4 * M * 8) + m * 32, 0);
 }
 
 template <int M>
 __device__ __forceinline__ double vget(const WaveWS& w, int v, int vl, int m) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(w.r, w.lane8 + vl * (M * kWave * 8),
-                                                                         (v * M + m) * kWave * 8, 0));
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(w.r, w.lane_off + vl * (4 * M * 8),
+                                                                         v * (4 * M * 8) + m * 32, 0));
 }
 
 template <int M>
@@ -127,7 +134,7 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
   const int64_t wave_doubles = (int64_t)nuts_nvec(a.d_max) * M * kWave;
   const int64_t n_waves = (a.n + 15) / 16;
   const WaveWS W{__builtin_amdgcn_make_buffer_rsrc(a.ws + wv * wave_doubles, 0, (int)(wave_doubles * 8), 0x00020000),
-                 lane * 8};
+                 (lane & 15) * nuts_nvec(a.d_max) * (4 * M * 8) + h * 8};
   int64_t* const tcur = reinterpret_cast<int64_t*>(a.ws + n_waves * wave_doubles);
 
   double q[M], p[M];
@@ -150,11 +157,11 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
   int d = 0, k = 0, Lsub = 1, udir = 0, ndraw = 0;
   bool lterm = false, rterm = false;
   double E_init = 0.0, E_max_now = 0.0, E_max_old = 0.0, pi_new = 1.0, pi_old = 1.0;
-  int table[kMaxDepth];
-#pragma unroll
-  for (int i = 0; i < kMaxDepth; ++i) table[i] = -1;
+  // save_index_table (:535) of this chain in LDS after P; the chain's 4 lanes keep identical copies
+  int* const table = reinterpret_cast<int*>(sP + MT * 4 * MT * kWave) +
+                     ((threadIdx.x / kWave) * 16 + (lane & 15)) * kMaxDepth;
   int64_t tpos = (REPLAY && live) ? tcur[c] : 0;        // replay tape cursor (persists across launches)
-  unsigned long long n_lf = 0, n_unst = 0, n_dmax = 0, n_tape = 0;
+  unsigned long long n_lf = 0, n_unst = 0, n_dmax = 0, n_tape = 0, n_steps = 0;
 
   auto draw = [&](bool direction) -> double {           // next random number of this chain (reference order)
     if constexpr (REPLAY) {
@@ -172,8 +179,7 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
 
   while (true) {
     // ================= transitions (ITER_END -> ITER_START -> SUB_START), converged reductions
-#pragma unroll 1
-    for (int pass = 0; pass < 2; ++pass) {
+    {
       const bool at_end = state == S_ITER_END;
       if (at_end) {                                     // samplers.py:786-791: q = live_point_q_old
         vload<M>(W, V_OLD_Q, 0, q);
@@ -190,11 +196,16 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
       }
       const bool starting = state == S_ITER_START;
       double kin = 0.0;
-      if (starting) {                                   // momentum (:565), dims h+4m
+      if (starting) {   // momentum (:565), dims h+4m, streamed to the boundaries: right = p, left = -p (:581-584)
         if constexpr (REPLAY) {
           const double* row = a.rp + (c * (int64_t)a.niter + (it - 1)) * a.D;
 #pragma unroll
-          for (int m = 0; m < M; ++m) p[m] = (h + 4 * m < a.D) ? row[h + 4 * m] : 0.0;
+          for (int m = 0; m < M; ++m) {
+            const double z = (h + 4 * m < a.D) ? row[h + 4 * m] : 0.0;
+            kin += z * (dim_minv<MT, GEN>(a, h + 4 * m) * z);
+            vput<M>(W, V_RIGHT_P, m, z);
+            vput<M>(W, V_LEFT_P, m, -z);
+          }
         } else {
 #pragma unroll
           for (int m = 0; m < M; m += 2) {
@@ -205,12 +216,17 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
               z0 *= a.pscale[min(d0, a.D - 1)];
               z1 *= a.pscale[min(d1, a.D - 1)];
             }
-            p[m] = d0 < a.D ? z0 : 0.0;
-            p[m + 1] = d1 < a.D ? z1 : 0.0;
+            z0 = d0 < a.D ? z0 : 0.0;
+            z1 = d1 < a.D ? z1 : 0.0;
+            kin += z0 * (dim_minv<MT, GEN>(a, d0) * z0);
+            kin += z1 * (dim_minv<MT, GEN>(a, d1) * z1);
+            vput<M>(W, V_RIGHT_P, m, z0);
+            vput<M>(W, V_LEFT_P, m, -z0);
+            vput<M>(W, V_RIGHT_P, m + 1, z1);
+            vput<M>(W, V_LEFT_P, m + 1, -z1);
+            __builtin_amdgcn_sched_barrier(0);
           }
         }
-#pragma unroll
-        for (int m = 0; m < M; ++m) kin += p[m] * (dim_minv<MT, GEN>(a, h + 4 * m) * p[m]);
       }
       kin = chain_sum4(kin);
       if (starting) {                                   // E_initial (:569), E/dE storage (:571-573)
@@ -222,14 +238,9 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
         }
         vstore<M>(W, V_OLD_Q, 0, q);                    // live_point_q_old = q (:577)
         gstore<MT>(W, V_OLD_G, 0, acc);
-        double np[M];
-#pragma unroll
-        for (int m = 0; m < M; ++m) np[m] = -p[m];
         vstore<M>(W, V_LEFT_Q, 0, q);                   // left = (q, -p), right = (q, p) (:581-584)
-        vstore<M>(W, V_LEFT_P, 0, np);
         gstore<MT>(W, V_LEFT_G, 0, acc);
         vstore<M>(W, V_RIGHT_Q, 0, q);
-        vstore<M>(W, V_RIGHT_P, 0, p);
         gstore<MT>(W, V_RIGHT_G, 0, acc);
         E_max_old = E_init;
         pi_old = 1.0;
@@ -238,25 +249,17 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
         ndraw = 0;
         state = S_SUB_START;
       }
-      if (state == S_SUB_START) {                       // one doubling (:595-626)
-        if (d > a.d_max - 1) {                          // :596-598 (reference aborts the run)
-          ++n_dmax;
-          state = S_ITER_END;
-        } else {
-#pragma unroll
-          for (int i = 0; i < kMaxDepth; ++i) table[i] = -1;
-          Lsub = 1 << d;
-          udir = (int)draw(true);                       // :608
-          const int b = udir == 0 ? V_RIGHT_Q : V_LEFT_Q;
-          vload<M>(W, 0, b, q);
-          vload<M>(W, 1, b, p);
-          gload<MT>(W, 2, b, acc);
-          k = 0;
-          state = S_READY;
-        }
+      if (state == S_SUB_START) {                       // one doubling (:595-626); d < d_max here
+        for (int i = 0; i <= a.d_max; ++i) table[i] = -1;
+        Lsub = 1 << d;
+        udir = (int)draw(true);                         // :608
+        const int b = udir == 0 ? V_RIGHT_Q : V_LEFT_Q;
+        vload<M>(W, 0, b, q);
+        vload<M>(W, 1, b, p);
+        gload<MT>(W, 2, b, acc);
+        k = 0;
+        state = S_READY;
       }
-      // a chain that hit d_max goes round once more (ITER_END -> ITER_START -> SUB_START)
-      if (pass == 0 && !__builtin_amdgcn_ballot_w64(state == S_ITER_END)) break;
     }
     if (!__builtin_amdgcn_ballot_w64(state != S_DONE)) break;
 
@@ -295,6 +298,7 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
     const double maha_pt = chain_sum4(mp1);
     const double E_tmp = 0.5 * (a.logc + (maha_pt + chain_sum4(kp1)));   // E (:618 / :643)
     if (act && h == 0) ++n_lf;
+    ++n_steps;
 
     // ================= process the new point
     bool reject = false, sub_end = false;
@@ -317,12 +321,8 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
         if (h == 0) ++n_unst;
       } else if ((mpt & 1) == 1) {                      // odd point: save (:654-658)
         int s = 0;
-#pragma unroll
-        for (int i = kMaxDepth - 1; i >= 0; --i)
-          if (table[i] == -1 && i <= a.d_max) s = i;      // find_next
-#pragma unroll
-        for (int i = 0; i < kMaxDepth; ++i)
-          if (i == s) table[i] = mpt;
+        while (s < a.d_max && table[s] != -1) ++s;      // find_next (a free slot always exists)
+        table[s] = mpt;
         vstore<M>(W, V_SLOTS, 2 * s, q);
         vstore<M>(W, V_SLOTS + 1, 2 * s, p);
       }
@@ -339,9 +339,8 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
       const bool doit = alive_chk && ci < ncheck;
       const int l = doit ? cp_point(mpt, ci) : 0;
       int s = 0;
-#pragma unroll
-      for (int i = 0; i < kMaxDepth; ++i)
-        if (table[i] == l) s = i;                       // retrieve_save_index (unique match)
+      if (doit)
+        while (s < a.d_max && table[s] != l) ++s;       // retrieve_save_index (unique match)
       double r_dot = 0.0, l_dot = 0.0;
       if (doit) {
 #pragma unroll
@@ -363,9 +362,7 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
           reject = true;
           alive_chk = false;
         } else if (l > 1 && release_fast(mpt, l)) {     // :735-736
-#pragma unroll
-          for (int i = 0; i < kMaxDepth; ++i)
-            if (i == s) table[i] = -1;
+          table[s] = -1;
         }
       }
     }
@@ -423,7 +420,14 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
       rterm = tr < 0.0;
       lterm = tl < 0.0;
       ++d;
-      state = (lterm && rterm) ? S_ITER_END : S_SUB_START;
+      if (lterm && rterm) {
+        state = S_ITER_END;
+      } else if (d > a.d_max - 1) {                     // :596-598 (the reference aborts the run)
+        ++n_dmax;
+        state = S_ITER_END;
+      } else {
+        state = S_SUB_START;
+      }
     }
   }
 
@@ -448,13 +452,14 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
     if (n_unst) atomicAdd(cs + HMC_CNT_UNSTABLE, n_unst);
     if (n_dmax) atomicAdd(cs + HMC_CNT_DMAX, n_dmax);
     if (n_tape) atomicAdd(cs + HMC_CNT_OOB_REJECT, n_tape);   // NUTS: replay tape exhausted
+    atomicAdd(cs + HMC_CNT_LEAPFROG_SQ, n_steps);               // NUTS: wave steps (lane utilisation)
   }
 }
 
 template <int MT, bool EXACT>
 hipError_t launch_nuts_mt2(const RandArgs& a, bool gen, bool replay, hipStream_t s) {
   const dim3 grid((unsigned)((a.n + 16 * kDenseWaves - 1) / (16 * kDenseWaves)));
-  const size_t lds = (size_t)MT * 4 * MT * kWave * sizeof(double);
+  const size_t lds = (size_t)MT * 4 * MT * kWave * sizeof(double) + kDenseWaves * 16 * kMaxDepth * sizeof(int);
   if (gen) {
     if (replay) k_nuts_iters<MT, EXACT, true, true><<<grid, 64 * kDenseWaves, lds, s>>>(a);
     else k_nuts_iters<MT, EXACT, true, false><<<grid, 64 * kDenseWaves, lds, s>>>(a);
