@@ -225,8 +225,9 @@ def _np_philox(ctr, key):
 
 
 def test_philox_normals_match_numpy_box_muller():
-    """The in-kernel fp64 Box-Muller (custom ~1-ulp log/sqrt/sincospi) agrees with NumPy's
-    libm-based Box-Muller on the same Philox words to a few ulp (absolute, scaled by the radius)."""
+    """The in-kernel fp64 Box-Muller (custom ~1-ulp log/sqrt/sincospi on 52-bit uniforms) agrees
+    with NumPy's libm-based Box-Muller on the same Philox words to a few ulp (absolute, scaled
+    by the radius)."""
     from hmc_amd import _lib as H
     L = H.lib()
     n, npairs, it, seed = 4096, 16, 5, 0x1234_5678_9abc
@@ -237,10 +238,10 @@ def test_philox_normals_match_numpy_box_muller():
     ks = np.tile(np.arange(npairs, dtype=np.uint64), n)
     ctr = np.stack([ks, np.full_like(ks, it), rows & np.uint64(0xFFFFFFFF), rows >> np.uint64(32)], axis=1)
     w = _np_philox(ctr, (seed & 0xFFFFFFFF, seed >> 32))
-    a = ((w[1] << np.uint64(21)) | (w[0] >> np.uint64(11))).astype(np.float64)
-    b = ((w[3] << np.uint64(21)) | (w[2] >> np.uint64(11))).astype(np.float64)
-    u1 = (a + 1.0) * 2.0 ** -53
-    u2 = b * 2.0 ** -53
+    a = ((w[1] << np.uint64(20)) | (w[0] >> np.uint64(12))).astype(np.float64)   # top 52 bits
+    b = ((w[3] << np.uint64(20)) | (w[2] >> np.uint64(12))).astype(np.float64)
+    u1 = 1.0 - a * 2.0 ** -52                                                     # (0, 1]
+    u2 = b * 2.0 ** -52                                                           # [0, 1)
     r = np.sqrt(-2.0 * np.log(u1))
     z0 = r * np.cos(2 * np.pi * u2)
     z1 = r * np.sin(2 * np.pi * u2)

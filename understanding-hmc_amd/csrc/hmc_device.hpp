@@ -19,15 +19,27 @@ namespace hmc {
 constexpr int kWave = 64;
 constexpr uint32_t kDrawSlot = 0x80000000u;  // counter.x for non-momentum draws (L, u, NUTS draws)
 
+// a ^ b ^ k in one VALU instruction: gfx950's three-input v_bitop3_b32 with truth table 0x96.
+// The key must be wave-uniform (every caller passes the seed from the kernel arguments): it is
+// an SGPR operand.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t k) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+  return r;
+}
+
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    // one v_mad_u64_u32 per 32x32->64 product (lo and hi words together)
+    // one v_mad_u64_u32 per 32x32->64 product (lo and hi words together), one v_bitop3 per xor pair
     const uint64_t p0 = (uint64_t)c.x * 0xD2511F53u;
     const uint64_t p1 = (uint64_t)c.z * 0xCD9E8D57u;
-    c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0);
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
+    c = make_uint4(xor3((uint32_t)(p1 >> 32), c.y, k0), (uint32_t)p1, xor3((uint32_t)(p0 >> 32), c.w, k1),
+                   (uint32_t)p0);
+    // key schedule on the SALU at the point of use: hoisted out of the chain loop it would hold
+    // 20 SGPRs and be spilled (v_readlane per round)
+    asm volatile("s_add_u32 %0, %0, 0x9E3779B9" : "+s"(k0));
+    asm volatile("s_add_u32 %0, %0, 0xBB67AE85" : "+s"(k1));
   }
   return c;
 }
@@ -59,24 +71,35 @@ __device__ __forceinline__ double rcp_nr(double d) {
   return __builtin_fma(r, e, r);
 }
 
-// log(x) for finite x > 0.
+// x*y + c with a compile-time constant c as an SGPR-pair operand of one v_fma_f64 (the compiler
+// otherwise copies each constant into the destination VGPRs and uses v_fmac: two instructions).
+__device__ __forceinline__ double fmac_k(double x, double y, double c) {
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "s"(c));
+  return r;
+}
+
+// log(x) for finite x > 0 (fdlibm e_log.c reduction; polynomials as Horner chains of
+// v_fma_f64 with the coefficients as SGPR operands).
 __device__ __forceinline__ double fast_log(double x) {
   int k = __builtin_amdgcn_frexp_exp(x);
   double m = __builtin_amdgcn_frexp_mant(x);       // [0.5, 1)
-  if (m < 0.70710678118654752440) {                 // -> [sqrt(1/2), sqrt(2))
-    m *= 2.0;
-    k -= 1;
-  }
+  const bool lo = m < 0.70710678118654752440;       // -> [sqrt(1/2), sqrt(2))
+  m = lo ? 2.0 * m : m;
+  k = lo ? k - 1 : k;
   const double f = m - 1.0;
-  const double hfsq = 0.5 * f * f;
   const double s = f * rcp_nr(2.0 + f);
   const double z = s * s, w = z * z;
-  const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 + w * 1.531383769920937332e-01));
-  const double t2 = z * (6.666666666666735130e-01 +
-                         w * (2.857142874366239149e-01 + w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
-  const double R = t2 + t1;
+  double t1 = fmac_k(w, 1.531383769920937332e-01, 2.222219843214978396e-01);   // Lg6, Lg4
+  t1 = fmac_k(w, t1, 3.999999999940941908e-01);                                   // Lg2
+  double t2 = fmac_k(w, 1.479819860511658591e-01, 1.818357216161805012e-01);    // Lg7, Lg5
+  t2 = fmac_k(w, t2, 2.857142874366239149e-01);                                   // Lg3
+  t2 = fmac_k(w, t2, 6.666666666666735130e-01);                                   // Lg1
+  const double R = __builtin_fma(z, t2, w * t1);
+  const double hfsq = (0.5 * f) * f;
   const double dk = (double)k;
-  return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
+  const double inner = __builtin_fma(s, hfsq + R, dk * 1.90821492927058770002e-10);
+  return __builtin_fma(dk, 6.93147180369123816490e-01, -((hfsq - inner) - f));
 }
 
 // sqrt(x) for x >= 0: v_rsq_f64 seed + one Goldschmidt/Newton refinement.
@@ -91,25 +114,27 @@ __device__ __forceinline__ double fast_sqrt(double x) {
   return x > 0.0 ? g : 0.0;
 }
 
-// sin(pi x), cos(pi x) for x in [0, 2].
+// sin(pi x), cos(pi x) for x in [0, 2] (fdlibm k_sin.c / k_cos.c kernels on |a| <= pi/4;
+// Horner chains of v_fma_f64 with SGPR coefficients).
 __device__ __forceinline__ void fast_sincospi(double x, double& sn, double& cs) {
   const double n = __builtin_rint(2.0 * x);
   const double r = __builtin_fma(-0.5, n, x);                    // exact, |r| <= 1/4
   const double a = __builtin_fma(r, 3.14159265358979311600e+00, r * 1.22464679914735317720e-16);
   const double z = a * a;
   const double v = z * a;
-  const double sr = 8.33333333332248946124e-03 +
-                    z * (-1.98412698298579493134e-04 +
-                         z * (2.75573137070700676789e-06 + z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)));
-  const double sa = a + v * (-1.66666666666666324348e-01 + z * sr);
-  const double cr = z * (4.16666666666666019037e-02 +
-                         z * (-1.38888888888741095749e-03 +
-                              z * (2.48015872894767294178e-05 +
-                                   z * (-2.75573143513906633035e-07 +
-                                        z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+  double sr = fmac_k(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08);   // S6, S5
+  sr = fmac_k(z, sr, 2.75573137070700676789e-06);                                     // S4
+  sr = fmac_k(z, sr, -1.98412698298579493134e-04);                                    // S3
+  sr = fmac_k(z, sr, 8.33333333332248946124e-03);                                     // S2
+  const double sa = __builtin_fma(v, fmac_k(z, sr, -1.66666666666666324348e-01), a);  // S1
+  double cr = fmac_k(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09);    // C6, C5
+  cr = fmac_k(z, cr, -2.75573143513906633035e-07);                                    // C4
+  cr = fmac_k(z, cr, 2.48015872894767294178e-05);                                     // C3
+  cr = fmac_k(z, cr, -1.38888888888741095749e-03);                                    // C2
+  cr = fmac_k(z, cr, 4.16666666666666019037e-02);                                     // C1
   const double hz = 0.5 * z;
   const double w = 1.0 - hz;
-  const double ca = w + (((1.0 - w) - hz) + z * cr);
+  const double ca = w + __builtin_fma(z * z, cr, (1.0 - w) - hz);
   const int q = ((int)n) & 3;                        // pi x = q*pi/2 + a
   const double s0 = (q & 1) ? ca : sa;
   const double c0 = (q & 1) ? sa : ca;
@@ -117,13 +142,21 @@ __device__ __forceinline__ void fast_sincospi(double x, double& sn, double& cs) 
   cs = ((q + 1) & 2) ? -c0 : c0;
 }
 
-// Two independent N(0,1) from one Philox block (fp64 Box–Muller).
+// [1, 2) with the top 52 bits of (hi:lo) as mantissa: 3 integer/bit VALU ops, no conversion.
+__device__ __forceinline__ double one_to_two(uint32_t lo, uint32_t hi) {
+  const uint32_t mlo = __builtin_amdgcn_alignbit(hi, lo, 12);   // low word of (hi:lo) >> 12
+  const uint32_t mhi = (hi >> 12) | 0x3FF00000u;
+  return __builtin_bit_cast(double, ((uint64_t)mhi << 32) | mlo);
+}
+
+// Two independent N(0,1) from one Philox block (fp64 Box–Muller on 52-bit uniforms:
+// u1 = 2 - d1 in (0, 1], angle 2*pi*(d2 - 1) in [0, 2*pi), all conversions exact).
 __device__ __forceinline__ void normal_pair(uint4 r, double& z0, double& z1) {
-  const double u1 = u53_open0(r.x, r.y);
-  const double u2 = u53(r.z, r.w);
+  const double u1 = 2.0 - one_to_two(r.x, r.y);
+  const double x2 = __builtin_fma(2.0, one_to_two(r.z, r.w), -2.0);
   const double rad = fast_sqrt(-2.0 * fast_log(u1));
   double s, c;
-  fast_sincospi(2.0 * u2, s, c);
+  fast_sincospi(x2, s, c);
   z0 = rad * c;
   z1 = rad * s;
 }

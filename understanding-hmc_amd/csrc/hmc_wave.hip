@@ -105,10 +105,16 @@ __global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
 
   // momentum and energy of the first iteration of this launch
   wave_momentum<K, GEN, REPLAY>(a, c, gc, a.it0, kk, pv, p);
-  double m0, k0;
+  double m0, k0, m0l;   // m0l: this lane's part of the potential of q (FAST mode bookkeeping)
   wave_partials<K, GEN>(a, kk, pv, q, p, m0, k0);
-  m0 = wave_sum_dpp(m0);
-  k0 = wave_sum_dpp(k0);
+  m0l = m0;
+  if constexpr (EXACT) {   // reference grouping: V and K summed separately
+    m0 = wave_sum_dpp(m0);
+    k0 = wave_sum_dpp(k0);
+  } else {                 // one reduction of V + K
+    k0 = wave_sum_dpp(m0 + k0);
+    m0 = 0.0;
+  }
   double E0 = 0.5 * (a.logc + (m0 + k0));
 
   // thinning bookkeeping without divisions: row = (it - wu)//thin, phase = (it - wu) % thin
@@ -203,23 +209,51 @@ __global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
           capp[2 * (l + 1) + 1] = a.D > 1 ? q[1] : q[0];
         }
       }
-    } else {
-      for (int l = 0; l < L; ++l) {
+    } else if (L > 0) {
+      // FAST: consecutive half kicks merged into one full kick, in shifted coordinates
+      // u = q - q0 (2 FMA per coordinate per step instead of 3; same integrator, other rounding)
+      double u[2 * K], dtc[2 * K], kh[2 * K], kfull[2 * K];
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
+      for (int j = 0; j < K; ++j) {
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int e = 2 * j + h;
-            const DimConst cc = slot_const<GEN>(a, kk[j], h, pv[j]);
-            const double co = GEN ? cc.hd * (cc.minv * cc.prec) : cc.hd;
-            const double ph = __builtin_fma(-co, q[e] - cc.q0, p[e]);
-            q[e] = __builtin_fma(cc.dt, ph, q[e]);
-            p[e] = __builtin_fma(-co, q[e] - cc.q0, ph);
-          }
+        for (int h = 0; h < 2; ++h) {
+          const int e = 2 * j + h;
+          const DimConst cc = slot_const<GEN>(a, kk[j], h, pv[j]);
+          kh[e] = -(GEN ? cc.hd * (cc.minv * cc.prec) : cc.hd);
+          kfull[e] = 2.0 * kh[e];
+          dtc[e] = cc.dt;
+          u[e] = GEN ? q[e] - cc.q0 : q[e];
+          p[e] = __builtin_fma(kh[e], u[e], p[e]);          // first half kick
         }
+      }
+      auto capture = [&](int l) {
         if (cap && lane == 0) {
-          capp[2 * (l + 1)] = q[0];
-          capp[2 * (l + 1) + 1] = a.D > 1 ? q[1] : q[0];
+          const double x0 = GEN ? u[0] + slot_const<GEN>(a, 0, 0, true).q0 : u[0];
+          const double x1 = a.D > 1 ? (GEN ? u[1] + slot_const<GEN>(a, 0, 1, true).q0 : u[1]) : x0;
+          capp[2 * (l + 1)] = x0;
+          capp[2 * (l + 1) + 1] = x1;
+        }
+      };
+      for (int l = 0; l + 1 < L; ++l) {
+#pragma unroll
+        for (int e = 0; e < 2 * K; ++e) {
+          u[e] = __builtin_fma(dtc[e], p[e], u[e]);         // drift
+          p[e] = __builtin_fma(kfull[e], u[e], p[e]);       // two half kicks merged
+        }
+        capture(l);
+      }
+#pragma unroll
+      for (int e = 0; e < 2 * K; ++e) {
+        u[e] = __builtin_fma(dtc[e], p[e], u[e]);           // last drift
+        p[e] = __builtin_fma(kh[e], u[e], p[e]);            // last half kick
+      }
+      capture(L - 1);
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int e = 2 * j + h;
+          q[e] = GEN ? u[e] + slot_const<GEN>(a, kk[j], h, pv[j]).q0 : u[e];
         }
       }
     }
@@ -231,11 +265,17 @@ __global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
       wave_momentum<K, GEN, REPLAY>(a, c, gc, it + 1, kk, pv, pn);
       kn = kin_partial<K, GEN>(a, kk, pv, pn);
     }
-    double m1, k1;
+    double m1, k1, m1l;
     wave_partials<K, GEN>(a, kk, pv, q, p, m1, k1);
-    m1 = wave_sum_dpp(m1);
-    k1 = wave_sum_dpp(k1);
-    kn = wave_sum_dpp(kn);
+    m1l = m1;
+    if constexpr (EXACT) {
+      m1 = wave_sum_dpp(m1);
+      k1 = wave_sum_dpp(k1);
+      kn = wave_sum_dpp(kn);
+    } else {
+      k1 = wave_sum_dpp(m1 + k1);
+      m1 = 0.0;
+    }
     const double E1 = 0.5 * (a.logc + (m1 + k1));
     const double dE = E1 - E0;                            // samplers.py:459
     const bool accept = (dE < 0.0) || (lnu < -dE);        // :462
@@ -265,8 +305,13 @@ __global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
     if (more) {
 #pragma unroll
       for (int e = 0; e < 2 * K; ++e) p[e] = pn[e];
-      m0 = accept ? m1 : m0;
-      E0 = 0.5 * (a.logc + (m0 + kn));
+      if constexpr (EXACT) {
+        m0 = accept ? m1 : m0;
+        E0 = 0.5 * (a.logc + (m0 + kn));
+      } else {                                            // V(q_next) + K(p_next) in one reduction
+        m0l = accept ? m1l : m0l;
+        E0 = 0.5 * (a.logc + wave_sum_dpp(m0l + kn));
+      }
     }
     if (post && ++phase == a.thin) {
       phase = 0;
