@@ -38,7 +38,7 @@ def test_struct_layouts():
     assert ctypes.sizeof(H.Kinetic) == 32
     assert ctypes.sizeof(H.Schedule) == 8 + 8 + 12 * 4 + 8
     assert ctypes.sizeof(H.Replay) == 48
-    assert ctypes.sizeof(H.State) == 9 * 8 + 8
+    assert ctypes.sizeof(H.State) == 9 * 8 + 8 + 2 * 8
 
 
 def test_invalid_arguments_map_to_reference_exceptions():

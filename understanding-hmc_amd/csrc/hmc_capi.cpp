@@ -93,6 +93,8 @@ hmc::RandArgs rand_args(const hmc_target* t, const hmc_kinetic* k, const hmc_sch
   a.q = st->q;
   a.Eprev = st->E_prev;
   a.qc = st->q_chain;
+  a.Lq = st->qc_rows > 0 ? (int)st->qc_rows : s->L_chain;
+  a.q_row0 = (int)st->qc_row0;
   a.Ec = st->E_chain;
   a.dEc = st->dE_chain;
   a.cnt = st->counters;
@@ -164,6 +166,7 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
                             hmc_state* st, void* stream) {
   if (hmc_status e = check_schedule(t, k, s, true)) return e;
   if (!st || !st->q || !st->E_prev) return fail(HMC_EINVAL, "null state");
+  if (st->qc_rows < 0 || st->qc_row0 < 0) return fail(HMC_EINVAL, "qc_rows, qc_row0 must be >= 0");
   if (s->iter_begin < 1 || s->iter_end < s->iter_begin || s->iter_end > s->n_iter + 1)
     return fail(HMC_EINVAL, "iteration range must satisfy 1 <= begin <= end <= Niter+1");
   const bool replay = s->rng_mode == HMC_RNG_REPLAY;
@@ -305,6 +308,25 @@ hmc_status hmc_variogram(const double* x, int64_t n_chains, int64_t chain_stride
   return hip_status(hmc::launch_variogram(x, n_chains, chain_stride, sample_stride, base, n, D, t0, t1, work, out,
                                           (hipStream_t)stream),
                     "hmc_variogram");
+}
+
+int64_t hmc_stream_work_size(int64_t n_chains, int32_t D, int32_t tmax) {
+  if (n_chains < 1 || D < 1 || (tmax != 8 && tmax != 16 && tmax != 32)) return 0;
+  return hmc::diag_stream_groups(n_chains) * (int64_t)tmax * D;
+}
+
+hmc_status hmc_stream_accumulate(const double* window, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
+                                 int32_t D, int32_t carry, int32_t rows, int64_t pos0, int32_t n_half, double* shift,
+                                 double* s1, double* s2, int32_t tmax, double* work, double* vsum, void* stream) {
+  if (!window || !shift || !s1 || !s2 || !work || !vsum || n_chains < 1 || D < 1 || rows < 0 || carry < 0 ||
+      n_half < 2 || pos0 < 0)
+    return fail(HMC_EINVAL, "bad arguments");
+  if (tmax != 8 && tmax != 16 && tmax != 32) return fail(HMC_EINVAL, "tmax must be 8, 16 or 32");
+  if (carry < (pos0 < tmax ? pos0 : tmax)) return fail(HMC_EINVAL, "carry must be >= min(tmax, pos0)");
+  if (rows == 0) return HMC_OK;
+  return hip_status(hmc::launch_stream_accum(window, n_chains, chain_stride, sample_stride, D, carry, rows, pos0,
+                                             n_half, shift, s1, s2, tmax, work, vsum, (hipStream_t)stream),
+                    "hmc_stream_accumulate");
 }
 
 }  // extern "C"

@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256, 1) void k_dense_iters(DenseArgs a) {
   }
   double Eprev = live ? a.Eprev[c] : 0.0;
   unsigned long long n_acc = 0, n_acc_wu = 0, n_lf = 0, n_lf2 = 0, n_oob = 0;
-  double* const qcb = a.qc ? a.qc + c * (int64_t)a.Lc * a.D : nullptr;
+  double* const qcb = a.qc ? a.qc + c * (int64_t)a.Lq * a.D : nullptr;
   // chain-0 trajectory capture (samplers.py:442-452): the wave holding global chain 0 (lane 0)
   const bool cap_wave = a.traj_q && uniform_i((int)(__builtin_amdgcn_readfirstlane((int)(gc & 0xffffffff)) == 0 &&
                                                     __builtin_amdgcn_readfirstlane((int)(gc >> 32)) == 0));
@@ -174,8 +174,8 @@ __global__ __launch_bounds__(256, 1) void k_dense_iters(DenseArgs a) {
 #pragma unroll
       for (int m = 0; m < M; ++m) q[m] = qi[m];
     }
-    if (live && write_row && qcb) {
-      double* rowp = qcb + row * a.D;
+    if (live && write_row && qcb && (uint64_t)(row - a.q_row0) < (uint64_t)a.Lq) {
+      double* rowp = qcb + (row - a.q_row0) * a.D;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         const int d = h + 4 * m;
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(256) void k_dense_init(DenseArgs a, int MT) {
   const double E0 = 0.5 * (a.logc + (maha + kin));
   for (int d = 0; d < a.D; ++d) {
     a.q[c * a.D + d] = qs[d];
-    if (a.qc) a.qc[c * (int64_t)a.Lc * a.D + d] = qs[d];
+    if (a.qc && a.q_row0 == 0) a.qc[c * (int64_t)a.Lq * a.D + d] = qs[d];
   }
   a.Eprev[c] = E0;
   if (a.Ec) a.Ec[c * (int64_t)a.Lc] = E0;

@@ -97,6 +97,16 @@ __global__ __launch_bounds__(256) void k_colsum_final(const double* partial, int
   out[c] = acc;
 }
 
+// out[c] += sum_k partial[k][c] (fixed order: deterministic; accumulates across calls).
+__global__ __launch_bounds__(256) void k_colsum_acc(const double* partial, int64_t nchunks, int64_t ncols,
+                                                    double* out) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncols) return;
+  double acc = 0.0;
+  for (int64_t k = 0; k < nchunks; ++k) acc += partial[k * ncols + c];
+  out[c] += acc;
+}
+
 // partial[chunk][t - t0][d] = sum over split chains j of the chunk of sum_s (x_j[s+t]-x_j[s])^2.
 __global__ __launch_bounds__(256) void k_variogram_partial(Src s, int t0, int t1, int64_t jchunk, double* partial) {
   __shared__ double red[4][kDimTile];
@@ -121,6 +131,81 @@ __global__ __launch_bounds__(256) void k_variogram_partial(Src s, int t0, int t1
     __syncthreads();
     if (rl == 0 && d < s.D)
       partial[((int64_t)blockIdx.x * nt + (t - t0)) * s.D + d] = ((red[0][dl] + red[1][dl]) + red[2][dl]) + red[3][dl];
+    __syncthreads();
+  }
+}
+
+// ---- streaming (windowed) split-chain statistics: q_chain never has to be stored whole.
+// Sample position p (0-based over q_chain[:, 1:, :]) lies in split half h = p / n at offset
+// s = p - h*n (positions >= 2n are not part of any split chain, utils.py:102-104).  A call
+// consumes `rows` new samples (positions pos0 ...) given a window whose first `carry` rows are
+// the samples just before pos0; carry >= min(T, pos0) keeps every lag t <= T exact.
+struct StreamArgs {
+  const double* x;
+  int64_t n_chains, chain_stride, sample_stride;
+  int D, carry, rows, n;
+  int64_t pos0;
+  double* shift;  // [n_chains][2][D] first sample of each half (variance shift)
+  double* s1;     // [n_chains][2][D] sum (x - shift)
+  double* s2;     // [n_chains][2][D] sum (x - shift)^2
+  double* vpart;  // [groups][T][D] partial variogram sums over this block's chains
+  int groups;
+};
+
+// Block = 4 chain lanes x 64 dims (lane = dim: coalesced rows).  Each thread walks its chains'
+// new rows once, with the last T samples in a register ring: per element, T differences.
+template <int T>
+__global__ __launch_bounds__(256) void k_stream_accum(StreamArgs a) {
+  __shared__ double red[4][kDimTile];
+  const int dl = threadIdx.x & (kDimTile - 1);
+  const int rl = threadIdx.x / kDimTile;
+  const int d = blockIdx.y * kDimTile + dl;
+  double v[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) v[t] = 0.0;
+  if (d < a.D) {
+    for (int64_t c = (int64_t)blockIdx.x * 4 + rl; c < a.n_chains; c += (int64_t)a.groups * 4) {
+      const double* xc = a.x + c * a.chain_stride + d;
+      double ring[T];
+#pragma unroll
+      for (int k = 0; k < T; ++k) ring[k] = (k < a.carry) ? xc[(int64_t)(a.carry - 1 - k) * a.sample_stride] : 0.0;
+      const int64_t o = c * 2 * a.D + d;
+      double sh[2] = {a.shift[o], a.shift[o + a.D]};
+      double m1[2] = {a.s1[o], a.s1[o + a.D]};
+      double m2[2] = {a.s2[o], a.s2[o + a.D]};
+      for (int i = 0; i < a.rows; ++i) {
+        const int64_t p = a.pos0 + i;
+        if (p >= 2 * (int64_t)a.n) break;
+        const double x = xc[(int64_t)(a.carry + i) * a.sample_stride];
+        const int h = p >= a.n ? 1 : 0;
+        const int sidx = (int)(p - (int64_t)h * a.n);
+        if (sidx == 0) sh[h] = x;
+        const double e = x - sh[h];
+        m1[h] += e;
+        m2[h] = __builtin_fma(e, e, m2[h]);
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          const double df = x - ring[t];
+          v[t] = (t < sidx) ? __builtin_fma(df, df, v[t]) : v[t];   // lag t+1 inside the same half
+        }
+#pragma unroll
+        for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
+        ring[0] = x;
+      }
+      a.shift[o] = sh[0];
+      a.shift[o + a.D] = sh[1];
+      a.s1[o] = m1[0];
+      a.s1[o + a.D] = m1[1];
+      a.s2[o] = m2[0];
+      a.s2[o + a.D] = m2[1];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    red[rl][dl] = v[t];
+    __syncthreads();
+    if (rl == 0 && d < a.D)
+      a.vpart[((int64_t)blockIdx.x * T + t) * a.D + d] = ((red[0][dl] + red[1][dl]) + red[2][dl]) + red[3][dl];
     __syncthreads();
   }
 }
@@ -160,6 +245,29 @@ hipError_t launch_rowsum(const double* x, int64_t n_outer, int64_t os, int64_t n
   k_rowsum_partial<<<grid, 256, 0, st>>>(r, work);
   if (hipError_t e = hipGetLastError()) return e;
   k_colsum_final<<<(unsigned)((D + 255) / 256), 256, 0, st>>>(work, nch, D, out);
+  return hipGetLastError();
+}
+
+int64_t diag_stream_groups(int64_t n_chains) {
+  const int64_t g = (n_chains + 3) / 4;
+  return g < 1024 ? (g < 1 ? 1 : g) : 1024;
+}
+
+hipError_t launch_stream_accum(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int D, int carry, int rows,
+                               int64_t pos0, int n, double* shift, double* s1, double* s2, int T, double* vpart,
+                               double* vsum, hipStream_t st) {
+  const int64_t groups = diag_stream_groups(n_chains);
+  StreamArgs a{x, n_chains, cs, ss, D, carry, rows, n, pos0, shift, s1, s2, vpart, (int)groups};
+  dim3 grid((unsigned)groups, (unsigned)((D + kDimTile - 1) / kDimTile));
+  switch (T) {
+    case 8: k_stream_accum<8><<<grid, 256, 0, st>>>(a); break;
+    case 16: k_stream_accum<16><<<grid, 256, 0, st>>>(a); break;
+    case 32: k_stream_accum<32><<<grid, 256, 0, st>>>(a); break;
+    default: return hipErrorInvalidValue;
+  }
+  if (hipError_t e = hipGetLastError()) return e;
+  const int64_t ncols = (int64_t)T * D;   // vsum[t][d] += sum over groups (accumulated across calls)
+  k_colsum_acc<<<(unsigned)((ncols + 255) / 256), 256, 0, st>>>(vpart, groups, ncols, vsum);
   return hipGetLastError();
 }
 

@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void k_random_init(RandArgs a) {
     if (pv[j]) {
       const bool v1 = 2 * kk[j] + 1 < a.D;
       store_pair(a.q + ln.c * (int64_t)a.D, kk[j], even, v1, q[2 * j], q[2 * j + 1]);
-      if (a.qc) store_pair(a.qc + ln.c * (int64_t)a.Lc * a.D, kk[j], even, v1, q[2 * j], q[2 * j + 1]);
+      if (a.qc && a.q_row0 == 0) store_pair(a.qc + ln.c * (int64_t)a.Lq * a.D, kk[j], even, v1, q[2 * j], q[2 * j + 1]);
     }
   }
   if (ln.leader) {
@@ -277,8 +277,8 @@ __global__ __launch_bounds__(256) void k_random_iters(RandArgs a) {
 #pragma unroll
       for (int e = 0; e < 2 * K; ++e) q[e] = qi[e];
     }
-    if (write_row && a.qc && !(a.dbg & 8)) {
-      double* rowp = a.qc + (ln.c * (int64_t)a.Lc + row) * a.D;
+    if (write_row && a.qc && !(a.dbg & 8) && (unsigned)(row - a.q_row0) < (unsigned)a.Lq) {
+      double* rowp = a.qc + (ln.c * (int64_t)a.Lq + (row - a.q_row0)) * a.D;
 #pragma unroll
       for (int j = 0; j < K; ++j)
         if (pv[j]) store_pair(rowp, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);

@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
   int rowbuf = -1, nbuf = 0;
   double* const Ec = a.Ec ? a.Ec + c * (int64_t)a.Lc : nullptr;
   double* const dEc = a.dEc ? a.dEc + c * (int64_t)a.Lc : nullptr;
-  double* const qcb = a.qc ? a.qc + c * (int64_t)a.Lc * a.D : nullptr;
+  double* const qcb = a.qc ? a.qc + c * (int64_t)a.Lq * a.D : nullptr;
   const bool cap_chain = a.traj_q && gc == 0 && !(a.dbg & 32);
   unsigned long long n_acc = 0, n_acc_wu = 0, n_lf = 0, n_lf2 = 0, n_oob = 0;
   int it_base = a.it0 - kWave, draw_L = 0;
@@ -283,8 +283,8 @@ __global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
 #pragma unroll
       for (int e = 0; e < 2 * K; ++e) q[e] = qi[e];
     }
-    if (write_row && qcb && !(a.dbg & 64)) {
-      double* rowp = qcb + (int64_t)row * a.D;
+    if (write_row && qcb && !(a.dbg & 64) && (unsigned)(row - a.q_row0) < (unsigned)a.Lq) {
+      double* rowp = qcb + (int64_t)(row - a.q_row0) * a.D;
 #pragma unroll
       for (int j = 0; j < K; ++j)
         if (pv[j]) store_pair(rowp, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);

@@ -136,9 +136,10 @@ def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
     return R.cpu().numpy(), n_eff
 
 
-def _ess_dim(Vt, var, n, m, complete):
+def _ess_dim(Vt, var, n, m, complete, truncate=False):
     """The termination loop of utils.py:130-157 given V_1..V_T (Vt[t-1]); None if more lags
-    are needed (and not all lags are available yet)."""
+    are needed (and not all lags are available yet).  truncate: the lags stop at len(Vt)
+    (streaming window), the sum ends there."""
     def V(t):
         return Vt[t - 1] if t - 1 < len(Vt) else None
     v1, v2 = V(1), V(2)
@@ -155,6 +156,8 @@ def _ess_dim(Vt, var, n, m, complete):
         while t < n - 2:
             vt = V(t + 2)
             if vt is None:
+                if truncate:
+                    break
                 return None
             rho.append(1 - vt / (2 * var))
             if ((t % 2) == 1) & ((rho[t] + rho[t + 1]) < 0):
@@ -203,3 +206,84 @@ def per_dim_mean_std(q_chain, group=None):
     _allreduce(m2, group)
     std = torch.sqrt(m2 / cnt)
     return mean.cpu().numpy(), std.cpu().numpy()
+
+
+# ---------------------------------------------------------------- streaming (windowed) statistics
+def _colsum(x, center=None):
+    """Per-dimension sum over the rows of a (rows, D) tensor (or of (x - center)^2): the HIP
+    kernel for device tensors; torch on host tensors (the CPU multi-process path)."""
+    if x.is_cuda:
+        return _rowsum(x.contiguous(), center)
+    return ((x - center) ** 2).sum(0) if center is not None else x.sum(0)
+
+
+def combine_split_stats(mean, std, vsum, n, group=None):
+    """R-hat and ESS (utils.py:109-157) from this rank's split-chain moments mean/std
+    (m_local, D), its variogram lag sums vsum (T, D) (vsum[t-1] = sum over its split chains of
+    sum_s (x[s+t] - x[s])^2, lags 1..T) and the half length n.  Every quantity is a sum over
+    split chains, so ranks all-reduce them (two rounds: B needs the global mean).  Lags stop
+    at T: the ESS sum ends there if the reference's criterion has not fired by then."""
+    dev = mean.device
+    m = int(_allreduce(torch.tensor([float(mean.shape[0])], dtype=torch.float64, device=dev), group).item())
+    assert m > 2                                                        # 2*Nchain, utils.py:85
+    s1 = torch.stack([_colsum(std), _colsum(mean)])
+    _allreduce(s1, group)
+    W = s1[0] / m                                                       # utils.py:112 (Q8)
+    mean_all = s1[1] / m                                                # :119
+    bsum = _allreduce(_colsum(mean, center=mean_all), group)
+    B = bsum * n / float(m - 1)                                         # :120
+    var = W * (n - 1) / float(n) + B / float(n)                         # :123
+    R = torch.sqrt(var / W)                                             # :126
+    v = _allreduce(vsum.clone(), group).cpu().numpy()
+    v = v[:max(2, min(v.shape[0], n - 1))]                              # lags t < n only
+    T, D = v.shape
+    lags = np.arange(1, T + 1)
+    Vt = v / (m * (n - lags))[:, None]                                  # utils.py:177
+    var_h = var.cpu().numpy()
+    n_eff = np.array([_ess_dim(Vt[:, i], var_h[i], n, m, complete=T >= n - 1, truncate=True)
+                      for i in range(D)])
+    return R.cpu().numpy(), n_eff
+
+
+class StreamingDiagnostics:
+    """convergence_stats (utils.py:77-159) of q_chain[:, 1:, :] without storing q_chain:
+    samples arrive in windows (hmc_stream_accumulate) and only per-chain/half moments plus
+    variogram lag sums for lags <= tmax are kept.  Exact for R-hat; ESS uses lags <= tmax
+    (the reference's sum stops earlier whenever its criterion fires within tmax).
+
+    n_samples = L_chain - 1 (rows after the dropped first row, Q16)."""
+
+    def __init__(self, n_chains, D, n_samples, tmax=16, device=None):
+        self.N, self.D, self.tmax = int(n_chains), int(D), int(tmax)
+        self.n = int(n_samples) // 2                                    # utils.py:102
+        assert self.n >= 2, "need at least 4 samples per chain"
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        z = lambda *s: torch.zeros(s, dtype=torch.float64, device=dev)  # noqa: E731
+        self.shift, self.s1, self.s2 = z(self.N, 2, D), z(self.N, 2, D), z(self.N, 2, D)
+        self.vsum = z(self.tmax, D)
+        L = H.lib()
+        self.work = z(max(1, L.hmc_stream_work_size(self.N, D, self.tmax)))
+        self.pos = 0                                                    # samples consumed
+
+    def update(self, window, carry, rows):
+        """window: (N, W, D) device tensor (any chain/sample strides, dims contiguous) whose rows
+        [0, carry) are the `carry` samples before the new ones and rows [carry, carry+rows) new."""
+        assert window.stride(2) == 1 and window.shape[0] == self.N and window.shape[2] == self.D
+        H.check(H.lib().hmc_stream_accumulate(window.data_ptr(), self.N, window.stride(0), window.stride(1), self.D,
+                                              int(carry), int(rows), self.pos, self.n, H.ptr(self.shift),
+                                              H.ptr(self.s1), H.ptr(self.s2), self.tmax, H.ptr(self.work),
+                                              H.ptr(self.vsum), _stream(window)), "hmc_stream_accumulate")
+        self.pos += int(rows)
+
+    def moments(self):
+        """Split-chain means and stds (ddof=1), (2N, D), chain-major like split_moments."""
+        n = float(self.n)
+        mean = self.shift + self.s1 / n
+        var = (self.s2 - self.s1 * self.s1 / n) / (n - 1.0)
+        return mean.reshape(2 * self.N, self.D), torch.sqrt(torch.clamp(var, min=0.0)).reshape(2 * self.N, self.D)
+
+    def finish(self, group=None):
+        assert self.pos >= 2 * self.n, "not all split-chain samples were fed"
+        mean, std = self.moments()
+        return combine_split_stats(mean, std, self.vsum, self.n, group)

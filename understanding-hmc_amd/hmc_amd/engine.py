@@ -76,6 +76,15 @@ class RandomEngine:
         self._replay = None
         self._streams = []
 
+    def set_chain_window(self, window, row0):
+        """Store q_chain rows [row0, row0 + window.shape[1]) into `window` (N, W, D) instead of a
+        whole-chain array (streaming diagnostics); other rows are not stored."""
+        assert window.shape[0] == self.N and window.shape[2] == self.D and window.is_contiguous()
+        self._window = window
+        self.S.q_chain = window.data_ptr()
+        self.S.qc_rows = window.shape[1]
+        self.S.qc_row0 = int(row0)
+
     def set_replay(self, p0, P, Ls, lnu):
         """Host-replayed draws (rng='replay'): p0 (N,D), p (N,Niter,D), L (N,Niter), log u (N,Niter)."""
         dev = self.device
@@ -105,6 +114,35 @@ class RandomEngine:
         """Iterations [it0, it1) of every chain in ONE fused kernel launch."""
         H.check(H.lib().hmc_random_iters(self.T, self.K, self.schedule(it0, it1), self._replay, self.S,
                                          self.stream()), "hmc_random_iters")
+
+    def run_streaming(self, diag, it_begin, it_end, step):
+        """Iterations [it_begin, it_end) in launches of `step`, with q_chain rows kept only in a
+        sliding device window that feeds `diag` (diagnostics.StreamingDiagnostics): memory is
+        O(N * (tmax + step/thin) * D) instead of O(N * L_chain * D).  Row 0 is not a sample of
+        the statistics (Q16); rows are fed once complete (a thinned row is final after its last
+        iteration)."""
+        N, D, T = self.N, self.D, diag.tmax
+        W = T + step // self.thin + 2
+        win = torch.zeros((N, W, D), dtype=torch.float64, device=self.device)
+        next_row = 1 + diag.pos            # next chain row the statistics need
+        row0_prev = None
+        for a in range(it_begin, it_end, step):
+            b = min(a + step, it_end)
+            carry = min(T, next_row - 1)
+            row0 = next_row - carry
+            if carry and row0_prev is not None:
+                off = row0 - row0_prev
+                win[:, :carry] = win[:, off:off + carry].clone()
+            self.set_chain_window(win, row0)
+            self.run(a, b)
+            done = self.L_chain if b - 1 == self.n_iter else max(0, (b - self.warm_up) // self.thin)
+            if done > next_row:
+                diag.update(win, carry, done - next_row)
+                next_row = done
+            row0_prev = row0
+        self.S.q_chain = H.ptr(self.q_chain)
+        self.S.qc_rows = 0
+        self.S.qc_row0 = 0
 
     def read_counters(self):
         return self.counters.cpu().numpy().astype(np.int64).sum(axis=0)
