@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget per process")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ess", action="store_true")
+    ap.add_argument("--stream-diag", action="store_true",
+                    help="no q_chain storage: R-hat/ESS from windowed streaming statistics inside the timed "
+                         "loop (config 4: D=1000 at 131072 chains/GPU)")
+    ap.add_argument("--tmax", type=int, default=16, help="streaming variogram lags")
     return ap.parse_args()
 
 
@@ -124,7 +128,7 @@ def main():
     from hmc_amd.engine import NutsEngine, RandomEngine
     from hmc_amd.target import MVNTarget
     from hmc_amd import _lib as H
-    from hmc_amd.diagnostics import convergence_stats
+    from hmc_amd.diagnostics import StreamingDiagnostics, convergence_stats
 
     D, N, S = a.dim, a.chains, a.iters_per_step
     W, K = a.warmup, a.steps
@@ -138,25 +142,34 @@ def main():
                          chain_offset=rank * N, store_chain=not a.no_ess, on_dmax="break", device=dev)
     else:
         eng = RandomEngine(tgt, N, n_iter, wu, 1, 5, 20, a.dt, rng="philox", seed=a.seed, fp_mode=a.fp_mode,
-                           chain_offset=rank * N, store_chain=not a.no_ess, device=dev)
+                           chain_offset=rank * N, store_chain=not (a.no_ess or a.stream_diag), device=dev)
+    sd = StreamingDiagnostics(N, D, eng.L_chain - 1, tmax=a.tmax, device=dev) if a.stream_diag else None
     rs = np.random.RandomState(a.seed + rank)
     eng.init(torch.as_tensor(rs.standard_normal((N, D)) * np.sqrt(2.0), device=dev))
     it = 1
+    def step(i0, evs=None):
+        if sd is not None:
+            eng.run_streaming(sd, i0, i0 + S, S, events=evs)
+        else:
+            if evs is not None:
+                evs[0].record(stream)
+            eng.run(i0, i0 + S)
+            if evs is not None:
+                evs[1].record(stream)
+
+    stream = torch.cuda.current_stream(dev)
     for _ in range(W):
-        eng.run(it, it + S)
+        step(it)
         it += S
     torch.cuda.synchronize(dev)
     c0 = eng.read_counters()
-    stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(K):
-        ev[k][0].record(stream)
-        eng.run(it, it + S)
-        ev[k][1].record(stream)
+        step(it, ev[k])
         it += S
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -180,15 +193,20 @@ def main():
     ess = None
     if not a.no_ess:
         grp = dist.group.WORLD if world > 1 else None
-        R, neff = convergence_stats(eng.q_chain[:, 1:, :], warm_up_num=0, thin_rate=1, group=grp)
+        if sd is not None:
+            R, neff = sd.finish(grp)
+        else:
+            R, neff = convergence_stats(eng.q_chain[:, 1:, :], warm_up_num=0, thin_rate=1, group=grp)
         ess = dict(ess_per_s_median=float(np.median(neff)) / t_max, ess_per_s_min=float(np.min(neff)) / t_max,
                    n_eff_median=float(np.median(neff)), rhat_median=float(np.median(R)),
-                   samples_per_chain=K * S)
+                   samples_per_chain=K * S,
+                   method=(f"streaming windows (tmax={a.tmax}) inside the timed loop" if sd is not None
+                           else "stored q_chain, after the timed loop"))
 
     if rank == 0:
         # algorithmic bytes of one launch (S iterations): per chain-iteration one q_chain row +
         # E + dE (8D + 16 B); per launch q and E_prev are read and written once (16D + 16 B)
-        row_bytes = 8 * D if eng.q_chain is not None else 0
+        row_bytes = 8 * D if (eng.q_chain is not None or sd is not None) else 0
         bytes_launch = N * (S * (row_bytes + 16) + 16 * D + 16)
         lf_launch = lf_local / K
         dense = a.rho != 0 or nuts

@@ -127,8 +127,9 @@ typedef struct hmc_state {
   int32_t* decision;
   int32_t n_save;
   int32_t traj_stride;     /* >= L_high (Random)                                              */
-  /* q_chain as a window (streaming diagnostics): the buffer holds qc_rows rows per chain, its
-   * first row being chain row qc_row0; rows outside are not stored.  0, 0 = the whole chain. */
+  /* q_chain as a circular window (streaming diagnostics): the buffer holds qc_rows rows per
+   * chain, chain row r >= qc_row0 is stored at row r % qc_rows; rows < qc_row0 are not stored.
+   * 0, 0 = the whole chain. */
   int64_t qc_rows;
   int64_t qc_row0;
 } hmc_state;
@@ -214,16 +215,18 @@ hmc_status hmc_variogram(const double* x, int64_t n_chains, int64_t chain_stride
 
 /* Streaming (windowed) split-chain statistics for runs whose q_chain does not fit: feed the
  * samples segment by segment.  Positions p index q_chain[:, 1:, :] (Q16); p lies in split half
- * h = p / n_half.  `window` row r (element [c*chain_stride + r*sample_stride + d]) holds position
- * pos0 - carry + r; rows [carry, carry + rows) are new.  carry >= min(tmax, pos0) keeps every
+ * h = p / n_half.  `window` is circular with `wrap` rows per chain (element [c*chain_stride +
+ * r*sample_stride + d]): the k-th sample from position pos0 - carry sits in row (slot0 + k) % wrap;
+ * the last `rows` of the carry + rows samples are new.  carry >= min(tmax, pos0) keeps every
  * variogram lag t <= tmax exact.  Accumulates per chain/half/dim shift (first sample), s1 =
  * sum (x - shift), s2 = sum (x - shift)^2 ([n_chains][2][D], zero-initialised) and
  * vsum[t-1][d] += sum over chains of sum (x[p] - x[p-t])^2 for lags t = 1..tmax (tmax in {8,16,32}).
  * Replaces the q_chain-wide passes of utils.py:88-126 and :161-179. */
 int64_t hmc_stream_work_size(int64_t n_chains, int32_t D, int32_t tmax);
 hmc_status hmc_stream_accumulate(const double* window, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
-                                 int32_t D, int32_t carry, int32_t rows, int64_t pos0, int32_t n_half, double* shift,
-                                 double* s1, double* s2, int32_t tmax, double* work, double* vsum, void* stream);
+                                 int32_t D, int32_t wrap, int32_t slot0, int32_t carry, int32_t rows, int64_t pos0,
+                                 int32_t n_half, double* shift, double* s1, double* s2, int32_t tmax, double* work,
+                                 double* vsum, void* stream);
 
 #ifdef __cplusplus
 }

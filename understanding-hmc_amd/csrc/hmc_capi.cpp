@@ -316,16 +316,17 @@ int64_t hmc_stream_work_size(int64_t n_chains, int32_t D, int32_t tmax) {
 }
 
 hmc_status hmc_stream_accumulate(const double* window, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
-                                 int32_t D, int32_t carry, int32_t rows, int64_t pos0, int32_t n_half, double* shift,
-                                 double* s1, double* s2, int32_t tmax, double* work, double* vsum, void* stream) {
+                                 int32_t D, int32_t wrap, int32_t slot0, int32_t carry, int32_t rows, int64_t pos0,
+                                 int32_t n_half, double* shift, double* s1, double* s2, int32_t tmax, double* work,
+                                 double* vsum, void* stream) {
   if (!window || !shift || !s1 || !s2 || !work || !vsum || n_chains < 1 || D < 1 || rows < 0 || carry < 0 ||
-      n_half < 2 || pos0 < 0)
+      n_half < 2 || pos0 < 0 || wrap < 1 || slot0 < 0 || slot0 >= wrap || carry + rows > wrap)
     return fail(HMC_EINVAL, "bad arguments");
   if (tmax != 8 && tmax != 16 && tmax != 32) return fail(HMC_EINVAL, "tmax must be 8, 16 or 32");
   if (carry < (pos0 < tmax ? pos0 : tmax)) return fail(HMC_EINVAL, "carry must be >= min(tmax, pos0)");
   if (rows == 0) return HMC_OK;
-  return hip_status(hmc::launch_stream_accum(window, n_chains, chain_stride, sample_stride, D, carry, rows, pos0,
-                                             n_half, shift, s1, s2, tmax, work, vsum, (hipStream_t)stream),
+  return hip_status(hmc::launch_stream_accum(window, n_chains, chain_stride, sample_stride, D, wrap, slot0, carry, rows,
+                                             pos0, n_half, shift, s1, s2, tmax, work, vsum, (hipStream_t)stream),
                     "hmc_stream_accumulate");
 }
 

@@ -174,8 +174,8 @@ __global__ __launch_bounds__(256, 1) void k_dense_iters(DenseArgs a) {
 #pragma unroll
       for (int m = 0; m < M; ++m) q[m] = qi[m];
     }
-    if (live && write_row && qcb && (uint64_t)(row - a.q_row0) < (uint64_t)a.Lq) {
-      double* rowp = qcb + (row - a.q_row0) * a.D;
+    if (live && write_row && qcb && row >= a.q_row0) {
+      double* rowp = qcb + (row % a.Lq) * a.D;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         const int d = h + 4 * m;

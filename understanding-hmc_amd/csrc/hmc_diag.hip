@@ -138,12 +138,13 @@ __global__ __launch_bounds__(256) void k_variogram_partial(Src s, int t0, int t1
 // ---- streaming (windowed) split-chain statistics: q_chain never has to be stored whole.
 // Sample position p (0-based over q_chain[:, 1:, :]) lies in split half h = p / n at offset
 // s = p - h*n (positions >= 2n are not part of any split chain, utils.py:102-104).  A call
-// consumes `rows` new samples (positions pos0 ...) given a window whose first `carry` rows are
-// the samples just before pos0; carry >= min(T, pos0) keeps every lag t <= T exact.
+// consumes `rows` new samples (positions pos0 ...) from a circular window of `wrap` rows per
+// chain: the k-th sample from position pos0 - carry sits in window row (slot0 + k) % wrap.
+// carry >= min(T, pos0) keeps every lag t <= T exact.
 struct StreamArgs {
   const double* x;
   int64_t n_chains, chain_stride, sample_stride;
-  int D, carry, rows, n;
+  int D, wrap, slot0, carry, rows, n;
   int64_t pos0;
   double* shift;  // [n_chains][2][D] first sample of each half (variance shift)
   double* s1;     // [n_chains][2][D] sum (x - shift)
@@ -151,6 +152,8 @@ struct StreamArgs {
   double* vpart;  // [groups][T][D] partial variogram sums over this block's chains
   int groups;
 };
+
+constexpr int kStreamChunk = 8;   // window rows loaded together (memory-level parallelism)
 
 // Block = 4 chain lanes x 64 dims (lane = dim: coalesced rows).  Each thread walks its chains'
 // new rows once, with the last T samples in a register ring: per element, T differences.
@@ -160,37 +163,50 @@ __global__ __launch_bounds__(256) void k_stream_accum(StreamArgs a) {
   const int dl = threadIdx.x & (kDimTile - 1);
   const int rl = threadIdx.x / kDimTile;
   const int d = blockIdx.y * kDimTile + dl;
+  const int64_t left = 2 * (int64_t)a.n - a.pos0;
+  const int rows = (int)(left < a.rows ? (left > 0 ? left : 0) : a.rows);
   double v[T];
 #pragma unroll
   for (int t = 0; t < T; ++t) v[t] = 0.0;
   if (d < a.D) {
     for (int64_t c = (int64_t)blockIdx.x * 4 + rl; c < a.n_chains; c += (int64_t)a.groups * 4) {
       const double* xc = a.x + c * a.chain_stride + d;
+      auto at = [&](int k) {             // k-th window sample (k < carry + rows)
+        int sl = a.slot0 + k;
+        sl = sl >= a.wrap ? sl - a.wrap : sl;
+        return xc[(int64_t)sl * a.sample_stride];
+      };
       double ring[T];
 #pragma unroll
-      for (int k = 0; k < T; ++k) ring[k] = (k < a.carry) ? xc[(int64_t)(a.carry - 1 - k) * a.sample_stride] : 0.0;
+      for (int k = 0; k < T; ++k) ring[k] = (k < a.carry) ? at(a.carry - 1 - k) : 0.0;
       const int64_t o = c * 2 * a.D + d;
       double sh[2] = {a.shift[o], a.shift[o + a.D]};
       double m1[2] = {a.s1[o], a.s1[o + a.D]};
       double m2[2] = {a.s2[o], a.s2[o + a.D]};
-      for (int i = 0; i < a.rows; ++i) {
-        const int64_t p = a.pos0 + i;
-        if (p >= 2 * (int64_t)a.n) break;
-        const double x = xc[(int64_t)(a.carry + i) * a.sample_stride];
-        const int h = p >= a.n ? 1 : 0;
-        const int sidx = (int)(p - (int64_t)h * a.n);
-        if (sidx == 0) sh[h] = x;
-        const double e = x - sh[h];
-        m1[h] += e;
-        m2[h] = __builtin_fma(e, e, m2[h]);
+      for (int i0 = 0; i0 < rows; i0 += kStreamChunk) {
+        double xs[kStreamChunk];
 #pragma unroll
-        for (int t = 0; t < T; ++t) {
-          const double df = x - ring[t];
-          v[t] = (t < sidx) ? __builtin_fma(df, df, v[t]) : v[t];   // lag t+1 inside the same half
+        for (int j = 0; j < kStreamChunk; ++j) xs[j] = (i0 + j < rows) ? at(a.carry + i0 + j) : 0.0;
+#pragma unroll
+        for (int j = 0; j < kStreamChunk; ++j) {
+          if (i0 + j >= rows) break;
+          const double x = xs[j];
+          const int64_t p = a.pos0 + i0 + j;
+          const int h = p >= a.n ? 1 : 0;
+          const int sidx = (int)(p - (int64_t)h * a.n);
+          if (sidx == 0) sh[h] = x;
+          const double e = x - sh[h];
+          m1[h] += e;
+          m2[h] = __builtin_fma(e, e, m2[h]);
+#pragma unroll
+          for (int t = 0; t < T; ++t) {
+            const double df = x - ring[t];
+            v[t] = (t < sidx) ? __builtin_fma(df, df, v[t]) : v[t];   // lag t+1 inside the same half
+          }
+#pragma unroll
+          for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
+          ring[0] = x;
         }
-#pragma unroll
-        for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
-        ring[0] = x;
       }
       a.shift[o] = sh[0];
       a.shift[o + a.D] = sh[1];
@@ -253,11 +269,11 @@ int64_t diag_stream_groups(int64_t n_chains) {
   return g < 1024 ? (g < 1 ? 1 : g) : 1024;
 }
 
-hipError_t launch_stream_accum(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int D, int carry, int rows,
-                               int64_t pos0, int n, double* shift, double* s1, double* s2, int T, double* vpart,
-                               double* vsum, hipStream_t st) {
+hipError_t launch_stream_accum(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int D, int wrap, int slot0,
+                               int carry, int rows, int64_t pos0, int n, double* shift, double* s1, double* s2, int T,
+                               double* vpart, double* vsum, hipStream_t st) {
   const int64_t groups = diag_stream_groups(n_chains);
-  StreamArgs a{x, n_chains, cs, ss, D, carry, rows, n, pos0, shift, s1, s2, vpart, (int)groups};
+  StreamArgs a{x, n_chains, cs, ss, D, wrap, slot0, carry, rows, n, pos0, shift, s1, s2, vpart, (int)groups};
   dim3 grid((unsigned)groups, (unsigned)((D + kDimTile - 1) / kDimTile));
   switch (T) {
     case 8: k_stream_accum<8><<<grid, 256, 0, st>>>(a); break;

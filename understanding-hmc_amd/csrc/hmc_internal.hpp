@@ -43,7 +43,7 @@ struct RandArgs {
   int32_t* traj_len;
   int32_t* decision;
   int n_save, traj_stride;
-  int Lq, q_row0;        // q_chain buffer: rows per chain and the chain row its first row holds
+  int Lq, q_row0;        // q_chain buffer: rows per chain (row r at r % Lq) and the first row stored
   int d_max, on_dmax;    // NUTS (hmc_nuts.hip)
   double* ws;            // NUTS per-chain workspace (vectors: live points, boundaries, save slots)
   const double* tape;    // NUTS replay tape [n][tape_stride] (directions / uniforms in consumption order)
@@ -96,9 +96,9 @@ hipError_t launch_rng_normals(uint32_t k0, uint32_t k1, int64_t chain0, int64_t 
 int64_t diag_rowsum_work(int64_t rows, int D);
 int64_t diag_variogram_work(int64_t n_chains, int D, int nlags);
 int64_t diag_stream_groups(int64_t n_chains);
-hipError_t launch_stream_accum(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int D, int carry, int rows,
-                               int64_t pos0, int n, double* shift, double* s1, double* s2, int T, double* vpart,
-                               double* vsum, hipStream_t st);
+hipError_t launch_stream_accum(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int D, int wrap, int slot0,
+                               int carry, int rows, int64_t pos0, int n, double* shift, double* s1, double* s2, int T,
+                               double* vpart, double* vsum, hipStream_t st);
 hipError_t launch_split_moments(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int64_t base, int n,
                                 int D, double* mean_out, double* std_out, hipStream_t st);
 hipError_t launch_rowsum(const double* x, int64_t n_outer, int64_t os, int64_t n_inner, int64_t is, int64_t base,

@@ -184,9 +184,9 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
       if (at_end) {                                     // samplers.py:786-791: q = live_point_q_old
         vload<M>(W, V_OLD_Q, 0, q);
         gload<MT>(W, V_OLD_G, 0, acc);
-        const int qrow = (it - a.wu) / a.thin - a.q_row0;
-        if (write_row_of(it) && a.qc && (unsigned)qrow < (unsigned)a.Lq) {
-          double* rowp = a.qc + (c * (int64_t)a.Lq + qrow) * a.D;
+        const int qrow = (it - a.wu) / a.thin;
+        if (write_row_of(it) && a.qc && qrow >= a.q_row0) {
+          double* rowp = a.qc + (c * (int64_t)a.Lq + qrow % a.Lq) * a.D;
 #pragma unroll
           for (int m = 0; m < M; ++m)
             if (h + 4 * m < a.D) rowp[h + 4 * m] = q[m];

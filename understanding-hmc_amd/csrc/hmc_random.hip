@@ -277,8 +277,8 @@ __global__ __launch_bounds__(256) void k_random_iters(RandArgs a) {
 #pragma unroll
       for (int e = 0; e < 2 * K; ++e) q[e] = qi[e];
     }
-    if (write_row && a.qc && !(a.dbg & 8) && (unsigned)(row - a.q_row0) < (unsigned)a.Lq) {
-      double* rowp = a.qc + (ln.c * (int64_t)a.Lq + (row - a.q_row0)) * a.D;
+    if (write_row && a.qc && !(a.dbg & 8) && row >= a.q_row0) {
+      double* rowp = a.qc + (ln.c * (int64_t)a.Lq + row % a.Lq) * a.D;
 #pragma unroll
       for (int j = 0; j < K; ++j)
         if (pv[j]) store_pair(rowp, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);

@@ -123,6 +123,7 @@ __global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
     row = (a.it0 - a.wu) / a.thin;
     phase = (a.it0 - a.wu) - row * a.thin;
   }
+  int qslot = row % a.Lq;                                // q_chain buffer row of `row` (circular window)
   double Ebuf = 0.0, dEbuf = 0.0;
   int rowbuf = -1, nbuf = 0;
   double* const Ec = a.Ec ? a.Ec + c * (int64_t)a.Lc : nullptr;
@@ -283,8 +284,8 @@ __global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
 #pragma unroll
       for (int e = 0; e < 2 * K; ++e) q[e] = qi[e];
     }
-    if (write_row && qcb && !(a.dbg & 64) && (unsigned)(row - a.q_row0) < (unsigned)a.Lq) {
-      double* rowp = qcb + (int64_t)(row - a.q_row0) * a.D;
+    if (write_row && qcb && !(a.dbg & 64) && row >= a.q_row0) {
+      double* rowp = qcb + (int64_t)qslot * a.D;
 #pragma unroll
       for (int j = 0; j < K; ++j)
         if (pv[j]) store_pair(rowp, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);
@@ -316,6 +317,7 @@ __global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
     if (post && ++phase == a.thin) {
       phase = 0;
       ++row;
+      if (++qslot == a.Lq) qslot = 0;
     }
   }
 

@@ -60,8 +60,9 @@ SYMBOLS = {
                                         ctypes.POINTER(Replay), ctypes.POINTER(State), c_dp]),
     "hmc_stream_work_size": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
     "hmc_stream_accumulate": (ctypes.c_int, [c_dp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
-                                             ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, c_dp,
-                                             c_dp, c_dp, ctypes.c_int32, c_dp, c_dp, c_dp]),
+                                             ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.c_int64, ctypes.c_int32, c_dp, c_dp, c_dp, ctypes.c_int32, c_dp,
+                                             c_dp, c_dp]),
     "hmc_nuts_workspace_size": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32]),
     "hmc_nuts_iters": (ctypes.c_int, [ctypes.POINTER(Target), ctypes.POINTER(Kinetic), ctypes.POINTER(Schedule),
                                       ctypes.POINTER(Replay), ctypes.POINTER(State), c_dp, c_dp]),

@@ -266,12 +266,14 @@ class StreamingDiagnostics:
         self.work = z(max(1, L.hmc_stream_work_size(self.N, D, self.tmax)))
         self.pos = 0                                                    # samples consumed
 
-    def update(self, window, carry, rows):
-        """window: (N, W, D) device tensor (any chain/sample strides, dims contiguous) whose rows
-        [0, carry) are the `carry` samples before the new ones and rows [carry, carry+rows) new."""
+    def update(self, window, carry, rows, slot0=0):
+        """window: (N, W, D) device tensor (any chain/sample strides, dims contiguous), circular:
+        the `carry` samples before the new ones and then the `rows` new samples sit in rows
+        slot0, slot0 + 1, ... (mod W)."""
         assert window.stride(2) == 1 and window.shape[0] == self.N and window.shape[2] == self.D
         H.check(H.lib().hmc_stream_accumulate(window.data_ptr(), self.N, window.stride(0), window.stride(1), self.D,
-                                              int(carry), int(rows), self.pos, self.n, H.ptr(self.shift),
+                                              window.shape[1], int(slot0), int(carry), int(rows), self.pos, self.n,
+                                              H.ptr(self.shift),
                                               H.ptr(self.s1), H.ptr(self.s2), self.tmax, H.ptr(self.work),
                                               H.ptr(self.vsum), _stream(window)), "hmc_stream_accumulate")
         self.pos += int(rows)

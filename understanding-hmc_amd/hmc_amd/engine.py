@@ -115,31 +115,35 @@ class RandomEngine:
         H.check(H.lib().hmc_random_iters(self.T, self.K, self.schedule(it0, it1), self._replay, self.S,
                                          self.stream()), "hmc_random_iters")
 
-    def run_streaming(self, diag, it_begin, it_end, step):
+    def run_streaming(self, diag, it_begin, it_end, step, events=None):
         """Iterations [it_begin, it_end) in launches of `step`, with q_chain rows kept only in a
-        sliding device window that feeds `diag` (diagnostics.StreamingDiagnostics): memory is
-        O(N * (tmax + step/thin) * D) instead of O(N * L_chain * D).  Row 0 is not a sample of
-        the statistics (Q16); rows are fed once complete (a thinned row is final after its last
-        iteration)."""
+        circular device window (chain row r in window row r % W) that feeds `diag`
+        (diagnostics.StreamingDiagnostics): memory O(N * (tmax + step/thin) * D) instead of
+        O(N * L_chain * D), no copies.  Row 0 is not a sample of the statistics (Q16); rows are
+        fed once complete (a thinned row is final after its last iteration).  May be called
+        repeatedly with consecutive ranges and the same `step`.
+        events: optional (start, end) CUDA events recorded around each sampler launch."""
         N, D, T = self.N, self.D, diag.tmax
         W = T + step // self.thin + 2
-        win = torch.zeros((N, W, D), dtype=torch.float64, device=self.device)
+        st = getattr(self, "_stream", None)
+        if st is None or st[0] is not diag or st[1].shape[1] != W:
+            st = [diag, torch.zeros((N, W, D), dtype=torch.float64, device=self.device)]
+            self._stream = st
+        win = st[1]
+        self.set_chain_window(win, 1)
         next_row = 1 + diag.pos            # next chain row the statistics need
-        row0_prev = None
         for a in range(it_begin, it_end, step):
             b = min(a + step, it_end)
-            carry = min(T, next_row - 1)
-            row0 = next_row - carry
-            if carry and row0_prev is not None:
-                off = row0 - row0_prev
-                win[:, :carry] = win[:, off:off + carry].clone()
-            self.set_chain_window(win, row0)
+            if events is not None:
+                events[0].record(torch.cuda.current_stream(self.device))
             self.run(a, b)
+            if events is not None:
+                events[1].record(torch.cuda.current_stream(self.device))
             done = self.L_chain if b - 1 == self.n_iter else max(0, (b - self.warm_up) // self.thin)
             if done > next_row:
-                diag.update(win, carry, done - next_row)
+                carry = min(T, next_row - 1)
+                diag.update(win, carry, done - next_row, slot0=(next_row - carry) % W)
                 next_row = done
-            row0_prev = row0
         self.S.q_chain = H.ptr(self.q_chain)
         self.S.qc_rows = 0
         self.S.qc_row0 = 0
