@@ -6,6 +6,8 @@ two calls of the hot path: `init()` (samplers.py:413-420) and `run(it0, it1)`
 (iterations of samplers.py:428-475, fused in one kernel launch).  HMC_sampler
 and bench.py are both thin layers over it.
 """
+import json
+
 import numpy as np
 import torch
 
@@ -147,6 +149,55 @@ class RandomEngine:
         self.S.q_chain = H.ptr(self.q_chain)
         self.S.qc_rows = 0
         self.S.qc_row0 = 0
+
+    # ---------------------------------------------------------------- checkpoint / resume
+    def _meta(self):
+        return dict(kind=type(self).__name__, N=self.N, D=self.D, n_iter=self.n_iter, warm_up=self.warm_up,
+                    thin=self.thin, L_low=self.L_low, L_high=self.L_high, seed=self.seed, rng=self.rng,
+                    fp_mode=self.fp_mode, chain_offset=self.chain_offset, d_max=self.d_max)
+
+    def save(self, path, it_next, include_chain=True, diag=None):
+        """Checkpoint after iteration it_next - 1 (.npz, no pickles).  Philox draws are keyed by
+        (seed, global chain, iteration), so a run resumed from it_next reproduces the
+        uninterrupted run bit for bit."""
+        torch.cuda.synchronize(self.device)
+        arr = dict(q=self.q, E_prev=self.E_prev, counters=self.counters)
+        if include_chain and self.q_chain is not None:
+            arr["q_chain"] = self.q_chain
+        if self.E_chain is not None:
+            arr["E_chain"], arr["dE_chain"] = self.E_chain, self.dE_chain
+        if getattr(self, "ws", None) is not None:
+            arr["ws"] = self.ws
+        if diag is not None:
+            arr.update(diag_shift=diag.shift, diag_s1=diag.s1, diag_s2=diag.s2, diag_vsum=diag.vsum)
+            st = getattr(self, "_stream", None)
+            if st is not None and st[0] is diag:
+                arr["window"] = st[1]                       # carry rows of the variogram lags
+        meta = dict(self._meta(), it_next=int(it_next), diag_pos=None if diag is None else diag.pos)
+        np.savez(path, meta=np.array(json.dumps(meta)), **{k: v.cpu().numpy() for k, v in arr.items()})
+
+    def restore(self, path, diag=None):
+        """Load a checkpoint written by save() into this (identically configured) engine;
+        returns the iteration to continue from."""
+        with np.load(path, allow_pickle=False) as z:
+            meta = json.loads(str(z["meta"]))
+            mine = self._meta()
+            bad = {k: (meta.get(k), v) for k, v in mine.items() if meta.get(k) != v}
+            if bad:
+                raise AssertionError(f"checkpoint does not match this engine: {bad}")
+            for k, t in (("q", self.q), ("E_prev", self.E_prev), ("counters", self.counters),
+                         ("q_chain", self.q_chain), ("E_chain", self.E_chain), ("dE_chain", self.dE_chain),
+                         ("ws", getattr(self, "ws", None))):
+                if t is not None and k in z.files:
+                    t.copy_(torch.as_tensor(z[k]).to(self.device))
+            if diag is not None:
+                for k, t in (("diag_shift", diag.shift), ("diag_s1", diag.s1), ("diag_s2", diag.s2),
+                             ("diag_vsum", diag.vsum)):
+                    t.copy_(torch.as_tensor(z[k]).to(self.device))
+                diag.pos = int(meta["diag_pos"])
+                if "window" in z.files:
+                    self._stream = [diag, torch.as_tensor(z["window"]).to(self.device)]
+        return int(meta["it_next"])
 
     def read_counters(self):
         return self.counters.cpu().numpy().astype(np.int64).sum(axis=0)
