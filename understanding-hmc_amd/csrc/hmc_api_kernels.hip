@@ -72,12 +72,15 @@ __global__ __launch_bounds__(256) void k_philox(uint4 c, uint32_t k0, uint32_t k
 
 __global__ __launch_bounds__(256) void k_rng_normals(uint32_t k0, uint32_t k1, int64_t chain0, int64_t n,
                                                      int it, int npairs, double* out) {
+  __shared__ double tab[kNormalTableDoubles];
+  init_normal_tables(tab);
+  __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * npairs) return;
   const int64_t row = i / npairs;
   const int k = (int)(i - row * npairs);
-  double z0, z1;
-  normal_pair(draw_block((uint32_t)k, (uint32_t)it, (uint64_t)(chain0 + row), k0, k1), z0, z1);
+  double z0, z1;   // the wave kernel's (table-driven) momentum transform
+  normal_pair_tab(draw_block((uint32_t)k, (uint32_t)it, (uint64_t)(chain0 + row), k0, k1), tab, z0, z1);
   out[2 * i] = z0;
   out[2 * i + 1] = z1;
 }

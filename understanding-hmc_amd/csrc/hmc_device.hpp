@@ -161,6 +161,84 @@ __device__ __forceinline__ void normal_pair(uint4 r, double& z0, double& z1) {
   z1 = rad * s;
 }
 
+// ---- table-driven Box–Muller (the wave kernel's momentum draws).  Per block, two small LDS
+// tables built once with the ~1-ulp kernels above:
+//   trig[i] = (cos, sin)(2*pi*i/256), i < 256            (4 KB)
+//   logt[j] = (1/c_j, -log(1/c_j)), c_j = centre of the j-th of 128 buckets of [0.5, 1)
+//             (the last bucket uses c = 1: log is then log1p(m - 1), relative-accurate near 1)
+// so that log and sincos reduce to short Horner chains around a table point.
+constexpr int kTrigN = 256, kLogN = 128;
+constexpr int kNormalTableDoubles = 2 * kTrigN + 2 * kLogN;
+
+// Every thread of the block calls this, then the block synchronises.
+__device__ __forceinline__ void init_normal_tables(double* tab) {
+  for (int i = threadIdx.x; i < kTrigN; i += blockDim.x) {
+    double sn, cs;
+    fast_sincospi((double)i * (1.0 / 128.0), sn, cs);
+    tab[2 * i] = cs;
+    tab[2 * i + 1] = sn;
+  }
+  for (int j = threadIdx.x; j < kLogN; j += blockDim.x) {
+    const double c = j == kLogN - 1 ? 1.0 : 0.5 + ((double)j + 0.5) * (0.5 / kLogN);
+    const double ic = j == kLogN - 1 ? 1.0 : rcp_nr(c);
+    tab[2 * kTrigN + 2 * j] = ic;
+    tab[2 * kTrigN + 2 * j + 1] = j == kLogN - 1 ? 0.0 : -fast_log(ic);
+  }
+}
+
+__device__ __forceinline__ double2 lds_pair(const double* p) { return *reinterpret_cast<const double2*>(p); }
+
+// log(u) for u in (0, 1] from the tables: u = 2^k m, m in [0.5, 1); bucket j = top 7 mantissa
+// bits; log m = L_j + log1p(m / c_j - 1) with |r| <= 2^-8 (series to r^7).
+__device__ __forceinline__ double table_log(double u, const double* tab) {
+  const int k = __builtin_amdgcn_frexp_exp(u);
+  const double m = __builtin_amdgcn_frexp_mant(u);
+  const uint32_t mhi = (uint32_t)(__builtin_bit_cast(uint64_t, m) >> 32);
+  const int j = (int)((mhi >> 13) & (kLogN - 1));
+  const double2 e = lds_pair(tab + 2 * kTrigN + 2 * j);
+  const double r = __builtin_fma(m, e.x, -1.0);
+  double pl = fmac_k(r, 1.0 / 7.0, -1.0 / 6.0);
+  pl = fmac_k(r, pl, 1.0 / 5.0);
+  pl = fmac_k(r, pl, -1.0 / 4.0);
+  pl = fmac_k(r, pl, 1.0 / 3.0);
+  pl = fmac_k(r, pl, -0.5);
+  const double l1p = __builtin_fma(r * r, pl, r);                       // log1p(r)
+  const double dk = (double)k;
+  return __builtin_fma(dk, 6.93147180369123816490e-01, e.y + __builtin_fma(dk, 1.90821492927058770002e-10, l1p));
+}
+
+// (cos, sin)(2*pi*(d - 1)) for d in [1, 2) holding 52 random mantissa bits: table point from the
+// top 8 bits, the rest delta in [0, 2*pi/256) by Taylor series (to delta^8).
+__device__ __forceinline__ void table_cossin(double d, const double* tab, double& cs, double& sn) {
+  const uint64_t bits = __builtin_bit_cast(uint64_t, d);
+  const uint32_t hi = (uint32_t)(bits >> 32);
+  const int i = (int)((hi >> 12) & (kTrigN - 1));
+  const double f = __builtin_bit_cast(double, bits & ~(0xFFull << 44)) - 1.0;    // [0, 2^-8), exact
+  const double dl = __builtin_fma(f, 6.28318530717958623200e+00, f * 2.44929359829470635445e-16);
+  const double z = dl * dl;
+  double ps = fmac_k(z, -1.0 / 5040.0, 1.0 / 120.0);
+  ps = fmac_k(z, ps, -1.0 / 6.0);
+  const double sd = __builtin_fma(dl * z, ps, dl);                       // sin(delta)
+  double pc = fmac_k(z, 1.0 / 40320.0, -1.0 / 720.0);
+  pc = fmac_k(z, pc, 1.0 / 24.0);
+  pc = fmac_k(z, pc, -0.5);
+  const double cd = __builtin_fma(z, pc, 1.0);                          // cos(delta)
+  const double2 t = lds_pair(tab + 2 * i);                              // (cos, sin)(theta_i)
+  cs = __builtin_fma(t.x, cd, -(t.y * sd));
+  sn = __builtin_fma(t.y, cd, t.x * sd);
+}
+
+// Two independent N(0,1) from one Philox block, table-driven Box–Muller (same uniforms as
+// normal_pair: u1 = 2 - d1 in (0, 1], angle 2*pi*(d2 - 1)).
+__device__ __forceinline__ void normal_pair_tab(uint4 r, const double* tab, double& z0, double& z1) {
+  const double u1 = 2.0 - one_to_two(r.x, r.y);
+  const double rad = fast_sqrt(-2.0 * table_log(u1, tab));
+  double c, s;
+  table_cossin(one_to_two(r.z, r.w), tab, c, s);
+  z0 = rad * c;
+  z1 = rad * s;
+}
+
 // Uniform integer in [lo, hi) from one word (multiply-shift; bias <= (hi-lo)/2^32).
 __device__ __forceinline__ int uniform_int(uint32_t w, int lo, int hi) {
   return lo + (int)(((uint64_t)w * (uint32_t)(hi - lo)) >> 32);

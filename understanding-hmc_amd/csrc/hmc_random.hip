@@ -192,7 +192,8 @@ __global__ __launch_bounds__(256) void k_random_iters(RandArgs a) {
         it_base = it;
         const uint4 r = draw_block(kDrawSlot, (uint32_t)(it + ln.s), gc, a.k0, a.k1);
         draw_L = uniform_int(r.x, a.L_low, a.L_high);
-        draw_lnu = log(u53(r.z, r.w));
+        const double u = u53(r.z, r.w);
+        draw_lnu = u > 0.0 ? fast_log(u) : -__builtin_inf();   // log(random()), :461
       }
       L = __shfl(draw_L, ln.base + (it - it_base), kWave);
       lnu = __shfl(draw_lnu, ln.base + (it - it_base), kWave);

@@ -59,7 +59,7 @@ __device__ __forceinline__ double kin_partial(const RandArgs& a, const int (&kk)
 
 template <int K, bool GEN, bool REPLAY>
 __device__ __forceinline__ void wave_momentum(const RandArgs& a, int64_t c, uint64_t gc, int it, const int (&kk)[K],
-                                              const bool (&pv)[K], double (&p)[2 * K]) {
+                                              const bool (&pv)[K], double (&p)[2 * K], const double* tab) {
   const bool even = (a.D & 1) == 0;
 #pragma unroll
   for (int j = 0; j < K; ++j) {
@@ -71,7 +71,7 @@ __device__ __forceinline__ void wave_momentum(const RandArgs& a, int64_t c, uint
         const double* row = a.rp + (c * (int64_t)a.niter + (it - 1)) * a.D;
         load_pair(row, kk[j], even, d + 1 < a.D, p[2 * j], p[2 * j + 1]);
       } else {
-        normal_pair(draw_block((uint32_t)kk[j], (uint32_t)it, gc, a.k0, a.k1), p[2 * j], p[2 * j + 1]);
+        normal_pair_tab(draw_block((uint32_t)kk[j], (uint32_t)it, gc, a.k0, a.k1), tab, p[2 * j], p[2 * j + 1]);
         if (GEN && a.pscale) {
           p[2 * j] *= a.pscale[d];
           if (d + 1 < a.D) p[2 * j + 1] *= a.pscale[d + 1];
@@ -83,7 +83,12 @@ __device__ __forceinline__ void wave_momentum(const RandArgs& a, int64_t c, uint
 }
 
 template <int K, bool EXACT, bool GEN, bool REPLAY>
-__global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
+__device__ __forceinline__ void wave_iters(const RandArgs& a) {
+  __shared__ double s_ntab[REPLAY ? 2 : kNormalTableDoubles];   // Box–Muller tables (Philox mode)
+  if constexpr (!REPLAY) {
+    init_normal_tables(s_ntab);
+    __syncthreads();
+  }
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t c = uniform_i(blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave));
   if (c >= a.n) return;                                  // whole wave, uniform
@@ -104,7 +109,7 @@ __global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
   __builtin_amdgcn_s_waitcnt(0x0F70);                    // retire state loads before the loop (vmcnt(0))
 
   // momentum and energy of the first iteration of this launch
-  wave_momentum<K, GEN, REPLAY>(a, c, gc, a.it0, kk, pv, p);
+  wave_momentum<K, GEN, REPLAY>(a, c, gc, a.it0, kk, pv, p, s_ntab);
   double m0, k0, m0l;   // m0l: this lane's part of the potential of q (FAST mode bookkeeping)
   wave_partials<K, GEN>(a, kk, pv, q, p, m0, k0);
   m0l = m0;
@@ -166,7 +171,8 @@ __global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
         it_base = it;
         const uint4 r = draw_block(kDrawSlot, (uint32_t)(it + lane), gc, a.k0, a.k1);
         draw_L = uniform_int(r.x, a.L_low, a.L_high);
-        draw_lnu = log(u53(r.z, r.w));
+        const double u = u53(r.z, r.w);
+        draw_lnu = u > 0.0 ? fast_log(u) : -__builtin_inf();   // log(random()), :461
       }
       L = __builtin_amdgcn_readlane(draw_L, it - it_base);
       lnu = readlane_d(draw_lnu, it - it_base);
@@ -263,7 +269,7 @@ __global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
     const bool more = it + 1 < a.it1;
     double kn = 0.0;
     if (more && !(a.dbg & 256)) {
-      wave_momentum<K, GEN, REPLAY>(a, c, gc, it + 1, kk, pv, pn);
+      wave_momentum<K, GEN, REPLAY>(a, c, gc, it + 1, kk, pv, pn, s_ntab);
       kn = kin_partial<K, GEN>(a, kk, pv, pn);
     }
     double m1, k1, m1l;
@@ -342,14 +348,32 @@ __global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
   }
 }
 
+// K = 1 (D <= 128, the headline shape) fits 64 VGPRs without spills: 8 waves per SIMD hide the
+// dependent-latency part of the loop (+4%); wider K keep the compiler's register budget.
+template <int K, bool EXACT, bool GEN, bool REPLAY>
+__global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
+  wave_iters<K, EXACT, GEN, REPLAY>(a);
+}
+
+template <bool EXACT, bool GEN, bool REPLAY>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_wave_iters_k1(RandArgs a) {
+  wave_iters<1, EXACT, GEN, REPLAY>(a);
+}
+
+template <int K, bool EXACT, bool GEN, bool REPLAY>
+void launch_wave_one(const RandArgs& a, dim3 grid, hipStream_t s) {
+  if constexpr (K == 1) k_wave_iters_k1<EXACT, GEN, REPLAY><<<grid, 256, 0, s>>>(a);
+  else k_wave_iters<K, EXACT, GEN, REPLAY><<<grid, 256, 0, s>>>(a);
+}
+
 template <int K, bool EXACT>
 hipError_t launch_wave_k2(const RandArgs& a, bool gen, bool replay, dim3 grid, hipStream_t s) {
   if (gen) {
-    if (replay) k_wave_iters<K, EXACT, true, true><<<grid, 256, 0, s>>>(a);
-    else k_wave_iters<K, EXACT, true, false><<<grid, 256, 0, s>>>(a);
+    if (replay) launch_wave_one<K, EXACT, true, true>(a, grid, s);
+    else launch_wave_one<K, EXACT, true, false>(a, grid, s);
   } else {
-    if (replay) k_wave_iters<K, EXACT, false, true><<<grid, 256, 0, s>>>(a);
-    else k_wave_iters<K, EXACT, false, false><<<grid, 256, 0, s>>>(a);
+    if (replay) launch_wave_one<K, EXACT, false, true>(a, grid, s);
+    else launch_wave_one<K, EXACT, false, false>(a, grid, s);
   }
   return hipGetLastError();
 }
