@@ -167,6 +167,8 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
   if (hmc_status e = check_schedule(t, k, s, true)) return e;
   if (!st || !st->q || !st->E_prev) return fail(HMC_EINVAL, "null state");
   if (st->qc_rows < 0 || st->qc_row0 < 0) return fail(HMC_EINVAL, "qc_rows, qc_row0 must be >= 0");
+  if ((st->qc_rows > 0 ? st->qc_rows : (int64_t)s->L_chain) * t->D * 8 > 0x7FFFFFFFll)
+    return fail(HMC_ENOTSUP, "one chain's q_chain rows exceed 2 GiB (use a streaming window)");
   if (s->iter_begin < 1 || s->iter_end < s->iter_begin || s->iter_end > s->n_iter + 1)
     return fail(HMC_EINVAL, "iteration range must satisfy 1 <= begin <= end <= Niter+1");
   const bool replay = s->rng_mode == HMC_RNG_REPLAY;

@@ -95,10 +95,11 @@ def lib():
     """Load libhmc.so once.  Raises (no fallback) when it is absent."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError(f"libhmc.so not found at {LIB_PATH}: build it with "
+        path = os.environ.get("HMC_LIB_PATH", LIB_PATH)      # A/B builds of the same tree
+        if not os.path.exists(path):
+            raise RuntimeError(f"libhmc.so not found at {path}: build it with "
                                f"`python -c 'import __graft_entry__ as g; g.build()'` (make in csrc/)")
-        L = ctypes.CDLL(LIB_PATH)
+        L = ctypes.CDLL(path)
         for name, (res, args) in SYMBOLS.items():
             fn = getattr(L, name)
             fn.restype = res
