@@ -1,9 +1,13 @@
+# Same-box A/B of two libhmc.so builds on the bench workload: A = lib/ab/libhmc_A.so (baseline),
+# B = the in-tree build.  Usage: bash scripts/gpu_ab.sh [extra bench args]
 set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/ab
-for F in 0 32 64 128 256 480; do
-  for L in 0 1; do
-    HMC_DEBUG_ABLATE=$F HMC_DEBUG_L=$L timeout -k 10 120 python bench.py --no-cpu-baseline --no-ess --steps 5 --chains 32768 > gpurun_out/ab/F${F}_L$L.log 2>&1 || exit $?
-  done
+for r in 1 2; do
+for v in A B; do
+  if [ $v = A ]; then export HMC_LIB_PATH=$GRAFT_REPO_ROOT/understanding-hmc_amd/lib/ab/libhmc_A.so; else unset HMC_LIB_PATH; fi
+  timeout -k 10 120 python bench.py --no-cpu-baseline --no-ess "$@" > gpurun_out/ab/fast_${v}_$r.log 2>&1 || exit $?
 done
+done
+grep -h -o '"value": [0-9.e+]*' gpurun_out/ab/fast_*_*.log
 echo done

@@ -2,6 +2,7 @@
 //
 // Validation mirrors the reference's asserts (samplers.py:331-348, :396) and returns
 // HMC_EINVAL instead of raising; the Python mirror re-raises AssertionError.
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -185,10 +186,22 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
   }
   const hmc::Layout lay = hmc::choose_layout(t->D, s->L_low, s->L_high);
   if (lay.K == 0) return fail(HMC_ENOTSUP, "D=%d too large for the diagonal kernels", t->D);
-  const hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
-  return hip_status(hmc::launch_random_iters(a, lay, s->fp_mode == HMC_MODE_EXACT, general_diag(t, k), replay,
-                                             (hipStream_t)stream),
-                    "hmc_random_iters");
+  hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
+  // the kernels keep per-launch tallies in 32 bits: Sum L^2 over one launch must stay < 2^31
+  // (only very long trajectories, e.g. L_high = 200, with thousands of iterations split here)
+  const int64_t lmax = std::max<int64_t>(std::max(s->L_high, 1), a.dbgL > 0 ? a.dbgL : 1);
+  const int64_t chunk = std::max<int64_t>(1, 0x7FFFFFFFll / (lmax * lmax));
+  for (int it = s->iter_begin; it < s->iter_end;) {
+    const int end = (int)std::min<int64_t>(s->iter_end, it + chunk);
+    a.it0 = it;
+    a.it1 = end;
+    if (hmc_status e = hip_status(hmc::launch_random_iters(a, lay, s->fp_mode == HMC_MODE_EXACT, general_diag(t, k),
+                                                           replay, (hipStream_t)stream),
+                                  "hmc_random_iters"))
+      return e;
+    it = end;
+  }
+  return HMC_OK;
 }
 
 int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max) {

@@ -82,7 +82,11 @@ __device__ __forceinline__ void wave_momentum(const RandArgs& a, int64_t c, uint
   }
 }
 
-template <int K, bool EXACT, bool GEN, bool REPLAY>
+// FULL: chain-0 trajectory capture and the ablation/debug hooks compiled in.  The production
+// variant (FULL = false) drops them: their pointers and flags are live across the iteration loop
+// and pushed the SGPR demand past the 8-waves/SIMD budget (spills to VGPR lanes cost one
+// v_readlane/v_writelane VALU slot each, ~45 per iteration).
+template <int K, bool EXACT, bool GEN, bool REPLAY, bool FULL>
 __device__ __forceinline__ void wave_iters(const RandArgs& a) {
   __shared__ double s_ntab[REPLAY ? 2 : kNormalTableDoubles];   // Box–Muller tables (Philox mode)
   if constexpr (!REPLAY) {
@@ -134,8 +138,10 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
   double* const Ec = a.Ec ? a.Ec + c * (int64_t)a.Lc : nullptr;
   double* const dEc = a.dEc ? a.dEc + c * (int64_t)a.Lc : nullptr;
   double* const qcb = a.qc ? a.qc + c * (int64_t)a.Lq * a.D : nullptr;
-  const bool cap_chain = a.traj_q && gc == 0 && !(a.dbg & 32);
-  unsigned long long n_acc = 0, n_acc_wu = 0, n_lf = 0, n_lf2 = 0, n_oob = 0;
+  const bool cap_chain = FULL && a.traj_q && gc == 0 && !(a.dbg & 32);
+  // per-launch tallies of one chain: (it1 - it0) <= 2^31 / L_high^2 is checked on the host, so
+  // 32-bit counters cannot wrap (half the SGPRs of 64-bit ones)
+  uint32_t n_acc = 0, n_acc_wu = 0, n_lf = 0, n_lf2 = 0, n_oob = 0;
   int it_base = a.it0 - kWave, draw_L = 0;
   double draw_lnu = 0.0;
 
@@ -177,7 +183,7 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
       L = __builtin_amdgcn_readlane(draw_L, it - it_base);
       lnu = readlane_d(draw_lnu, it - it_base);
     }
-    if (a.dbgL >= 0) L = a.dbgL;                          // diagnostics: forced trajectory length
+    if (FULL && a.dbgL >= 0) L = a.dbgL;                          // diagnostics: forced trajectory length
     L = uniform_i(L);
 
     // chain-0 trajectory capture (samplers.py:442-452)
@@ -268,7 +274,7 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     // next iteration's momentum (keyed by it+1) so its kinetic energy joins this reduction
     const bool more = it + 1 < a.it1;
     double kn = 0.0;
-    if (more && !(a.dbg & 256)) {
+    if (more && !(FULL && (a.dbg & 256))) {
       wave_momentum<K, GEN, REPLAY>(a, c, gc, it + 1, kk, pv, pn, s_ntab);
       kn = kin_partial<K, GEN>(a, kk, pv, pn);
     }
@@ -286,11 +292,11 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     const double E1 = 0.5 * (a.logc + (m1 + k1));
     const double dE = E1 - E0;                            // samplers.py:459
     const bool accept = (dE < 0.0) || (lnu < -dE);        // :462
-    if (!accept && !(a.dbg & 128)) {
+    if (!accept && !(FULL && (a.dbg & 128))) {
 #pragma unroll
       for (int e = 0; e < 2 * K; ++e) q[e] = qi[e];
     }
-    if (write_row && qcb && !(a.dbg & 64) && row >= a.q_row0) {
+    if (write_row && qcb && !(FULL && (a.dbg & 64)) && row >= a.q_row0) {
       double* rowp = qcb + (int64_t)qslot * a.D;
 #pragma unroll
       for (int j = 0; j < K; ++j)
@@ -305,7 +311,7 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     } else if (it < a.i_oob) {
       ++n_oob;
     }
-    const unsigned long long Lp = L > 0 ? (unsigned long long)L : 0ull;
+    const uint32_t Lp = L > 0 ? (uint32_t)L : 0u;
     n_lf += Lp;
     n_lf2 += Lp * Lp;
     // advance
@@ -339,31 +345,37 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     a.Eprev[c] = Eprev;
     if (a.cnt) {   // per-wave counts into one of HMC_COUNTER_SLOTS rows (no single-address hot spot)
       unsigned long long* cs = a.cnt + (c & (HMC_COUNTER_SLOTS - 1)) * HMC_NCOUNTERS;
-      if (n_acc) atomicAdd(cs + HMC_CNT_ACCEPT, n_acc);
-      if (n_acc_wu) atomicAdd(cs + HMC_CNT_ACCEPT_WU, n_acc_wu);
-      if (n_lf) atomicAdd(cs + HMC_CNT_LEAPFROG, n_lf);
-      if (n_lf2) atomicAdd(cs + HMC_CNT_LEAPFROG_SQ, n_lf2);
-      if (n_oob) atomicAdd(cs + HMC_CNT_OOB_REJECT, n_oob);
+      if (n_acc) atomicAdd(cs + HMC_CNT_ACCEPT, (unsigned long long)n_acc);
+      if (n_acc_wu) atomicAdd(cs + HMC_CNT_ACCEPT_WU, (unsigned long long)n_acc_wu);
+      if (n_lf) atomicAdd(cs + HMC_CNT_LEAPFROG, (unsigned long long)n_lf);
+      if (n_lf2) atomicAdd(cs + HMC_CNT_LEAPFROG_SQ, (unsigned long long)n_lf2);
+      if (n_oob) atomicAdd(cs + HMC_CNT_OOB_REJECT, (unsigned long long)n_oob);
     }
   }
 }
 
 // K = 1 (D <= 128, the headline shape) fits 64 VGPRs without spills: 8 waves per SIMD hide the
 // dependent-latency part of the loop (+4%); wider K keep the compiler's register budget.
-template <int K, bool EXACT, bool GEN, bool REPLAY>
+template <int K, bool EXACT, bool GEN, bool REPLAY, bool FULL>
 __global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
-  wave_iters<K, EXACT, GEN, REPLAY>(a);
+  wave_iters<K, EXACT, GEN, REPLAY, FULL>(a);
 }
 
-template <bool EXACT, bool GEN, bool REPLAY>
+template <bool EXACT, bool GEN, bool REPLAY, bool FULL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_wave_iters_k1(RandArgs a) {
-  wave_iters<1, EXACT, GEN, REPLAY>(a);
+  wave_iters<1, EXACT, GEN, REPLAY, FULL>(a);
 }
 
 template <int K, bool EXACT, bool GEN, bool REPLAY>
 void launch_wave_one(const RandArgs& a, dim3 grid, hipStream_t s) {
-  if constexpr (K == 1) k_wave_iters_k1<EXACT, GEN, REPLAY><<<grid, 256, 0, s>>>(a);
-  else k_wave_iters<K, EXACT, GEN, REPLAY><<<grid, 256, 0, s>>>(a);
+  const bool full = a.traj_q != nullptr || a.dbg != 0 || a.dbgL >= 0;
+  if constexpr (K == 1) {
+    if (full) k_wave_iters_k1<EXACT, GEN, REPLAY, true><<<grid, 256, 0, s>>>(a);
+    else k_wave_iters_k1<EXACT, GEN, REPLAY, false><<<grid, 256, 0, s>>>(a);
+  } else {
+    if (full) k_wave_iters<K, EXACT, GEN, REPLAY, true><<<grid, 256, 0, s>>>(a);
+    else k_wave_iters<K, EXACT, GEN, REPLAY, false><<<grid, 256, 0, s>>>(a);
+  }
 }
 
 template <int K, bool EXACT>
