@@ -50,6 +50,9 @@ def parse():
                     help="no q_chain storage: R-hat/ESS from windowed streaming statistics inside the timed "
                          "loop (config 4: D=1000 at 131072 chains/GPU)")
     ap.add_argument("--tmax", type=int, default=16, help="streaming variogram lags")
+    ap.add_argument("--no-order-tiles", action="store_true",
+                    help="dense targets: MFMA tiles in chain order (several iterations per launch) instead of "
+                         "L-ordered tiles (one launch per iteration, chains sorted by trajectory length)")
     return ap.parse_args()
 
 
@@ -142,7 +145,8 @@ def main():
                          chain_offset=rank * N, store_chain=not a.no_ess, on_dmax="break", device=dev)
     else:
         eng = RandomEngine(tgt, N, n_iter, wu, 1, 5, 20, a.dt, rng="philox", seed=a.seed, fp_mode=a.fp_mode,
-                           chain_offset=rank * N, store_chain=not (a.no_ess or a.stream_diag), device=dev)
+                           chain_offset=rank * N, store_chain=not (a.no_ess or a.stream_diag), device=dev,
+                           order_tiles=not a.no_order_tiles)
     sd = StreamingDiagnostics(N, D, eng.L_chain - 1, tmax=a.tmax, device=dev) if a.stream_diag else None
     rs = np.random.RandomState(a.seed + rank)
     eng.init(torch.as_tensor(rs.standard_normal((N, D)) * np.sqrt(2.0), device=dev))

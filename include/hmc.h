@@ -132,6 +132,11 @@ typedef struct hmc_state {
    * 0, 0 = the whole chain. */
   int64_t qc_rows;
   int64_t qc_row0;
+  /* Dense targets, Random sampler: scratch of hmc_random_workspace_size() bytes for L-ordered
+   * tiles (each iteration, chains are counting-sorted by trajectory length so that the 16
+   * chains sharing an MFMA tile integrate the same number of steps; results are unchanged).
+   * NULL = tiles in chain order (several iterations fused per launch).  Ignored for DIAG. */
+  int32_t* order;
 } hmc_state;
 
 const char* hmc_version(void);
@@ -150,6 +155,9 @@ hmc_status hmc_chain_init(const hmc_target* t, const hmc_kinetic* k, const hmc_s
 hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s,
                             const hmc_replay* r /* NULL for Philox */, hmc_state* st, void* stream);
 
+/* Bytes of the optional hmc_state.order scratch for hmc_random_iters on this target
+ * (0 for diagonal targets, which need none). */
+int64_t hmc_random_workspace_size(const hmc_target* t, int64_t n_chains);
 /* Bytes of device workspace hmc_nuts_iters needs for n_chains chains (tree vectors: live
  * points, both boundaries, d_max+1 save slots; replay-tape cursors).  0 if unsupported. */
 int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max);

@@ -38,7 +38,7 @@ def test_struct_layouts():
     assert ctypes.sizeof(H.Kinetic) == 32
     assert ctypes.sizeof(H.Schedule) == 8 + 8 + 12 * 4 + 8
     assert ctypes.sizeof(H.Replay) == 48
-    assert ctypes.sizeof(H.State) == 9 * 8 + 8 + 2 * 8
+    assert ctypes.sizeof(H.State) == 9 * 8 + 8 + 2 * 8 + 8
 
 
 def test_invalid_arguments_map_to_reference_exceptions():
@@ -70,3 +70,14 @@ def test_no_cpu_fallback_when_library_missing(tmp_path, monkeypatch):
     with pytest.raises(RuntimeError, match="libhmc.so not found"):
         H.lib()
     importlib.reload(H)
+
+
+def test_random_workspace_size_query(monkeypatch):
+    """hmc_random_workspace_size: no scratch for diagonal targets; dense targets take an int32
+    chain order + two 256-bin histograms (host-only query, no GPU call)."""
+    from hmc_amd import _lib as H
+    monkeypatch.setattr(H, "_lib", None)     # argtypes bound to this module's structure classes
+    L = H.lib()
+    assert L.hmc_random_workspace_size(ctypes.byref(H.Target(100, H.HMC_TARGET_DIAG, None, None, 0.0)), 1000) == 0
+    assert L.hmc_random_workspace_size(ctypes.byref(H.Target(100, H.HMC_TARGET_DENSE, None, None, 0.0)), 1000) == (1000 + 512) * 4
+    assert L.hmc_random_workspace_size(None, 1000) == 0

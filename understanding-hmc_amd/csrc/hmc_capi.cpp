@@ -74,6 +74,7 @@ hmc::RandArgs rand_args(const hmc_target* t, const hmc_kinetic* k, const hmc_sch
   a.L_high = s->L_high;
   a.it0 = s->iter_begin;
   a.it1 = s->iter_end;
+  a.ntiles = (s->n_chains + 15) / 16;
   a.i_oob = (int)(s->warm_up - (int64_t)s->L_chain * s->thin);  // rejections at i < i_oob index < -L_chain
   a.k0 = (uint32_t)s->seed;
   a.k1 = (uint32_t)(s->seed >> 32);
@@ -180,9 +181,23 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
   if (t->kind == HMC_TARGET_DENSE) {
     if (!hmc::dense_tiles(t->D)) return fail(HMC_ENOTSUP, "dense target: D=%d > 128 not supported", t->D);
     const hmc::Layout lay{0, 0, 0, (t->D + 1) / 2};
-    const hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
-    return hip_status(hmc::launch_dense_iters(a, s->fp_mode == HMC_MODE_EXACT, replay, (hipStream_t)stream),
-                      "hmc_random_iters(dense)");
+    hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
+    const bool exact = s->fp_mode == HMC_MODE_EXACT;
+    if (!st->order || a.traj_q || !hmc::dense_order_ok(a))
+      return hip_status(hmc::launch_dense_iters(a, exact, replay, (hipStream_t)stream), "hmc_random_iters(dense)");
+    // L-ordered tiles: one launch per iteration, chains counting-sorted by that iteration's L
+    for (int it = s->iter_begin; it < s->iter_end; ++it) {
+      if (hmc_status e = hip_status(hmc::launch_dense_order(a, it, replay, st->order, (hipStream_t)stream),
+                                    "hmc_random_iters(dense order)"))
+        return e;
+      a.it0 = it;
+      a.it1 = it + 1;
+      a.order = st->order;
+      if (hmc_status e = hip_status(hmc::launch_dense_iters(a, exact, replay, (hipStream_t)stream),
+                                    "hmc_random_iters(dense)"))
+        return e;
+    }
+    return HMC_OK;
   }
   const hmc::Layout lay = hmc::choose_layout(t->D, s->L_low, s->L_high);
   if (lay.K == 0) return fail(HMC_ENOTSUP, "D=%d too large for the diagonal kernels", t->D);
@@ -202,6 +217,11 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
     it = end;
   }
   return HMC_OK;
+}
+
+int64_t hmc_random_workspace_size(const hmc_target* t, int64_t n_chains) {
+  if (!t || n_chains < 0 || t->kind != HMC_TARGET_DENSE) return 0;
+  return hmc::dense_order_ints(n_chains) * (int64_t)sizeof(int32_t);
 }
 
 int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max) {

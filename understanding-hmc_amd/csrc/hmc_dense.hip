@@ -15,6 +15,8 @@
 // gradient; the 4 lanes of a chain reduce with two xor-shuffles.
 // Chains of one wave can have different trajectory lengths L: the wave runs max L and
 // finished chains are masked (their gradient is recomputed at an unchanged q, bit-identical).
+#include <algorithm>
+
 #include "hmc_device.hpp"
 #include "hmc_internal.hpp"
 #include "hmc_dense_ops.hpp"
@@ -31,8 +33,17 @@ __global__ __launch_bounds__(256, 1) void k_dense_iters(DenseArgs a) {
 
   const int lane = threadIdx.x & (kWave - 1);
   const int h = lane >> 4;
-  const int64_t c = ((int64_t)blockIdx.x * kDenseWaves + (threadIdx.x / kWave)) * 16 + (lane & 15);
-  const bool live = c < a.n;
+  unsigned long long n_acc = 0, n_acc_wu = 0, n_lf = 0, n_lf2 = 0, n_oob = 0;
+  // Persistent waves: P is staged into LDS once per block and the block's waves stride over the
+  // 16-chain tiles.  With a.order (L-ordered tiles, one iteration per launch) tile t holds the
+  // chains order[16t .. 16t+15], which share (up to bucket edges) one trajectory length, so no
+  // lane idles through another chain's longer trajectory.
+  const int64_t wave_id = (int64_t)blockIdx.x * kDenseWaves + (threadIdx.x / kWave);
+  const int64_t n_waves = (int64_t)gridDim.x * kDenseWaves;
+  for (int64_t tile = wave_id; tile < a.ntiles; tile += n_waves) {
+  const int64_t slot = tile * 16 + (lane & 15);
+  const bool live = slot < a.n;
+  const int64_t c = a.order ? (live ? (int64_t)a.order[slot] : 0) : slot;
   const uint64_t gc = (uint64_t)(a.chain_offset + c);
   double q[M], p[M], qi[M];
   d4 acc[MT];
@@ -42,9 +53,9 @@ __global__ __launch_bounds__(256, 1) void k_dense_iters(DenseArgs a) {
     q[m] = (live && d < a.D) ? a.q[c * a.D + d] : 0.0;
   }
   double Eprev = live ? a.Eprev[c] : 0.0;
-  unsigned long long n_acc = 0, n_acc_wu = 0, n_lf = 0, n_lf2 = 0, n_oob = 0;
   double* const qcb = a.qc ? a.qc + c * (int64_t)a.Lq * a.D : nullptr;
-  // chain-0 trajectory capture (samplers.py:442-452): the wave holding global chain 0 (lane 0)
+  // chain-0 trajectory capture (samplers.py:442-452): the wave holding global chain 0 (lane 0;
+  // capture runs never use a.order)
   const bool cap_wave = a.traj_q && uniform_i((int)(__builtin_amdgcn_readfirstlane((int)(gc & 0xffffffff)) == 0 &&
                                                     __builtin_amdgcn_readfirstlane((int)(gc >> 32)) == 0));
 
@@ -203,14 +214,14 @@ __global__ __launch_bounds__(256, 1) void k_dense_iters(DenseArgs a) {
     if (live && d < a.D) a.q[c * a.D + d] = q[m];
   }
   if (live && h == 0) a.Eprev[c] = Eprev;
+  }   // tile loop
   n_acc = wave_sum_u64(n_acc);
   n_acc_wu = wave_sum_u64(n_acc_wu);
   n_lf = wave_sum_u64(n_lf);
   n_lf2 = wave_sum_u64(n_lf2);
   n_oob = wave_sum_u64(n_oob);
   if (lane == 0 && a.cnt) {
-    const int64_t wv = (int64_t)blockIdx.x * kDenseWaves + (threadIdx.x / kWave);
-    unsigned long long* cs = a.cnt + (wv & (HMC_COUNTER_SLOTS - 1)) * HMC_NCOUNTERS;
+    unsigned long long* cs = a.cnt + (wave_id & (HMC_COUNTER_SLOTS - 1)) * HMC_NCOUNTERS;
     if (n_acc) atomicAdd(cs + HMC_CNT_ACCEPT, n_acc);
     if (n_acc_wu) atomicAdd(cs + HMC_CNT_ACCEPT_WU, n_acc_wu);
     if (n_lf) atomicAdd(cs + HMC_CNT_LEAPFROG, n_lf);
@@ -262,9 +273,67 @@ __global__ __launch_bounds__(256) void k_dense_init(DenseArgs a, int MT) {
   if (a.dEc) a.dEc[c * (int64_t)a.Lc] = 0.0;
 }
 
+// ---- L-ordered tiles (one iteration per launch): counting sort of the chains by this
+// iteration's trajectory length, so each 16-chain tile runs (nearly) one L.  The draws are the
+// ones k_dense_iters makes (samplers.py:441); the order only decides which lanes a chain
+// occupies, never a value it computes.
+constexpr int kOrderBins = 256;
+
+__device__ __forceinline__ int dense_bin(const DenseArgs& a, int64_t c, int it, bool replay) {
+  int L;
+  if (replay) {
+    L = a.rL[c * (int64_t)a.niter + (it - 1)];
+  } else {
+    const uint4 r = draw_block(kDrawSlot, (uint32_t)it, (uint64_t)(a.chain_offset + c), a.k0, a.k1);
+    L = uniform_int(r.x, a.L_low, a.L_high);
+  }
+  return min(max(L - a.L_low, 0), a.L_high - a.L_low - 1);
+}
+
+__global__ __launch_bounds__(256) void k_order_hist(DenseArgs a, int it, bool replay, int32_t* hist) {
+  __shared__ int cnt[kOrderBins];
+  const int nb = a.L_high - a.L_low;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) cnt[b] = 0;
+  __syncthreads();
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < a.n) atomicAdd(&cnt[dense_bin(a, c, it, replay)], 1);
+  __syncthreads();
+  for (int b = threadIdx.x; b < nb; b += blockDim.x)
+    if (cnt[b]) atomicAdd(&hist[b], cnt[b]);
+}
+
+__global__ __launch_bounds__(256) void k_order_scatter(DenseArgs a, int it, bool replay, const int32_t* hist,
+                                                       int32_t* cursor, int32_t* order) {
+  __shared__ int cnt[kOrderBins], base[kOrderBins];
+  const int nb = a.L_high - a.L_low;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) cnt[b] = 0;
+  __syncthreads();
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int bin = 0, rank = 0;
+  if (c < a.n) {
+    bin = dense_bin(a, c, it, replay);
+    rank = atomicAdd(&cnt[bin], 1);
+  }
+  if (threadIdx.x == 0) {            // exclusive prefix of the global histogram
+    int run = 0;
+    for (int b = 0; b < nb; ++b) {
+      base[b] = run;
+      run += hist[b];
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < nb; b += blockDim.x)
+    if (cnt[b]) base[b] += atomicAdd(&cursor[b], cnt[b]);
+  __syncthreads();
+  if (c < a.n) order[base[bin] + rank] = (int32_t)c;
+}
+
+
 template <int MT, bool EXACT>
 hipError_t launch_dense_mt2(const DenseArgs& a, bool gen, bool replay, hipStream_t s) {
-  const dim3 grid((unsigned)((a.n + 16 * kDenseWaves - 1) / (16 * kDenseWaves)));
+  // one block per CU (the LDS copy of P limits residency to one), a few rounds of tiles each
+  const int64_t blocks = (a.ntiles + kDenseWaves - 1) / kDenseWaves;
+  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)device_cus())));
   const size_t lds = (size_t)MT * 4 * MT * kWave * sizeof(double);
   if (gen) {
     if (replay) k_dense_iters<MT, EXACT, true, true><<<grid, 64 * kDenseWaves, lds, s>>>(a);
@@ -283,6 +352,18 @@ hipError_t launch_dense_mt(const DenseArgs& a, bool exact, bool gen, bool replay
 
 }  // namespace
 
+int device_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int v = 0;
+    cache[dev] = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v
+                                                                                                                : 256;
+  }
+  return cache[dev];
+}
+
 int dense_tiles(int D) {
   const int mt = (D + 15) / 16;
   if (mt <= 1) return 1;
@@ -298,6 +379,20 @@ hipError_t launch_dense_init(const DenseArgs& a, bool replay, hipStream_t s) {
   const int MT = dense_tiles(a.D);
   if (replay) k_dense_init<true><<<grid, 256, 0, s>>>(a, MT);
   else k_dense_init<false><<<grid, 256, 0, s>>>(a, MT);
+  return hipGetLastError();
+}
+
+int64_t dense_order_ints(int64_t n) { return n + 2 * kOrderBins; }
+
+bool dense_order_ok(const DenseArgs& a) { return a.L_high - a.L_low <= kOrderBins && a.n < (1ll << 31); }
+
+hipError_t launch_dense_order(const DenseArgs& a, int it, bool replay, int32_t* ws, hipStream_t s) {
+  int32_t* hist = ws + a.n;
+  int32_t* cursor = hist + kOrderBins;
+  if (hipError_t e = hipMemsetAsync(hist, 0, 2 * kOrderBins * sizeof(int32_t), s)) return e;
+  const dim3 grid((unsigned)((a.n + 255) / 256));
+  k_order_hist<<<grid, 256, 0, s>>>(a, it, replay, hist);
+  k_order_scatter<<<grid, 256, 0, s>>>(a, it, replay, hist, cursor, ws);
   return hipGetLastError();
 }
 

@@ -51,6 +51,8 @@ struct RandArgs {
   int dbg;               // ablation flags (HMC_DEBUG_ABLATE env; 0 in normal runs)
   int dbgL;              // forced trajectory length (HMC_DEBUG_L env; -1 in normal runs)
   unsigned long long* stamps;  // diagnostic phase timers (HMC_DEBUG_STAMPS env; null in normal runs)
+  const int32_t* order;  // dense: tile slot -> chain (L-ordered tiles) or null (slot = chain)
+  int64_t ntiles;        // dense: 16-chain tiles
 };
 
 // Dense-precision (correlated MVN) kernels take the same argument block; `prec` is then the
@@ -68,6 +70,10 @@ hipError_t launch_random_iters(const RandArgs& a, const Layout& lay, bool exact,
 hipError_t launch_wave_iters(const RandArgs& a, int K, bool exact, bool gen, bool replay, hipStream_t s);
 hipError_t launch_dense_init(const DenseArgs& a, bool replay, hipStream_t s);
 hipError_t launch_dense_iters(const DenseArgs& a, bool exact, bool replay, hipStream_t s);
+int64_t dense_order_ints(int64_t n);   // int32 scratch of the L-ordering (order[n] + histograms)
+bool dense_order_ok(const DenseArgs& a);
+hipError_t launch_dense_order(const DenseArgs& a, int it, bool replay, int32_t* ws, hipStream_t s);
+int device_cus();
 
 
 // Row-wise API kernels (hmc_api_kernels.hip).

@@ -47,7 +47,7 @@ class State(ctypes.Structure):
     _fields_ = [("q", c_dp), ("E_prev", c_dp), ("q_chain", c_dp), ("E_chain", c_dp), ("dE_chain", c_dp),
                 ("counters", c_dp), ("traj_q", c_dp), ("traj_len", c_dp), ("decision", c_dp),
                 ("n_save", ctypes.c_int32), ("traj_stride", ctypes.c_int32),
-                ("qc_rows", ctypes.c_int64), ("qc_row0", ctypes.c_int64)]
+                ("qc_rows", ctypes.c_int64), ("qc_row0", ctypes.c_int64), ("order", c_dp)]
 
 
 # Exported symbols (tests check every one of these is present; keep in sync with include/hmc.h)
@@ -63,6 +63,7 @@ SYMBOLS = {
                                              ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                              ctypes.c_int64, ctypes.c_int32, c_dp, c_dp, c_dp, ctypes.c_int32, c_dp,
                                              c_dp, c_dp]),
+    "hmc_random_workspace_size": (ctypes.c_int64, [ctypes.POINTER(Target), ctypes.c_int64]),
     "hmc_nuts_workspace_size": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32]),
     "hmc_nuts_iters": (ctypes.c_int, [ctypes.POINTER(Target), ctypes.POINTER(Kinetic), ctypes.POINTER(Schedule),
                                       ctypes.POINTER(Replay), ctypes.POINTER(State), c_dp, c_dp]),

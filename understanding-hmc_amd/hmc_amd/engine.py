@@ -21,7 +21,7 @@ def _dev(a, device, dtype=torch.float64):
 class RandomEngine:
     def __init__(self, target, n_chains, n_iter, warm_up, thin, L_low, L_high, dt, cov_p=None, rng="philox",
                  seed=0, fp_mode="fast", chain_offset=0, store_chain=True, store_energy=True, n_save=0,
-                 device=None, dense=False):
+                 device=None, dense=False, order_tiles=True):
         self.t = target
         self.D = D = target.D
         self.N = int(n_chains)
@@ -75,6 +75,11 @@ class RandomEngine:
         self.S = H.State(H.ptr(self.q), H.ptr(self.E_prev), H.ptr(self.q_chain), H.ptr(self.E_chain),
                          H.ptr(self.dE_chain), H.ptr(self.counters), H.ptr(self.traj), H.ptr(self.traj_len),
                          H.ptr(self.decision), self.n_save, self.traj_stride)
+        # dense targets: scratch for L-ordered MFMA tiles (chains sorted by trajectory length
+        # every iteration; same results, no lane idling through a longer trajectory)
+        nbytes = H.lib().hmc_random_workspace_size(self.T, self.N) if order_tiles else 0
+        self._order = torch.zeros((nbytes + 3) // 4, dtype=torch.int32, device=dev) if nbytes > 0 else None
+        self.S.order = H.ptr(self._order)
         self._replay = None
         self._streams = []
 
