@@ -25,8 +25,11 @@ namespace hmc {
 
 namespace {
 
-template <int MT, bool EXACT, bool GEN, bool REPLAY>
-__global__ __launch_bounds__(256, 1) void k_dense_iters(DenseArgs a) {
+// WAVES waves per block, one block per CU (the LDS copy of P); WAVES = 4: one wave per SIMD
+// with the whole 512-register file.
+template <int MT, bool EXACT, bool GEN, bool REPLAY, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVES / 4, WAVES / 4)))
+void k_dense_iters(DenseArgs a) {
   constexpr int M = 4 * MT;
   extern __shared__ double sP[];
   stage_precision<MT>(a, sP);
@@ -38,19 +41,26 @@ __global__ __launch_bounds__(256, 1) void k_dense_iters(DenseArgs a) {
   // 16-chain tiles.  With a.order (L-ordered tiles, one iteration per launch) tile t holds the
   // chains order[16t .. 16t+15], which share (up to bucket edges) one trajectory length, so no
   // lane idles through another chain's longer trajectory.
-  const int64_t wave_id = (int64_t)blockIdx.x * kDenseWaves + (threadIdx.x / kWave);
-  const int64_t n_waves = (int64_t)gridDim.x * kDenseWaves;
+  const int64_t wave_id = (int64_t)blockIdx.x * WAVES + (threadIdx.x / kWave);
+  const int64_t n_waves = (int64_t)gridDim.x * WAVES;
   for (int64_t tile = wave_id; tile < a.ntiles; tile += n_waves) {
   const int64_t slot = tile * 16 + (lane & 15);
   const bool live = slot < a.n;
   const int64_t c = a.order ? (live ? (int64_t)a.order[slot] : 0) : slot;
   const uint64_t gc = (uint64_t)(a.chain_offset + c);
-  double q[M], p[M], qi[M];
+  // a.q keeps the chain's state at the start of the current iteration (written back on every
+  // acceptance), so a rejection reloads it instead of holding a copy in registers
+  double q[M], p[M];
   d4 acc[MT];
+  double* const qrow = a.q + c * a.D;
+  double* const qh = qrow + h;           // dims h + 4m: constant offsets 32m from one base
+  // dim h + 4m < D  <=>  m < mfull, or m == mfull and h < D % 4: a scalar test for all but one m
+  // (a per-lane compare for every m is loop-invariant and gets hoisted into 28 SGPR-pair masks)
+  const int mfull = uniform_i(a.D >> 2), mrem = a.D & 3;
+  auto dim_ok = [&](int m) -> bool { return m < mfull || (m == mfull && h < mrem); };
 #pragma unroll
   for (int m = 0; m < M; ++m) {
-    const int d = h + 4 * m;
-    q[m] = (live && d < a.D) ? a.q[c * a.D + d] : 0.0;
+    q[m] = (live && dim_ok(m)) ? qh[4 * m] : 0.0;
   }
   double Eprev = live ? a.Eprev[c] : 0.0;
   double* const qcb = a.qc ? a.qc + c * (int64_t)a.Lq * a.D : nullptr;
@@ -62,24 +72,25 @@ __global__ __launch_bounds__(256, 1) void k_dense_iters(DenseArgs a) {
   for (int it = a.it0; it < a.it1; ++it) {
     // ---- momentum (samplers.py:431): dims h+4m; Philox pairs (m, m+1) keyed by slot h + 8*(m/2)
     if constexpr (REPLAY) {
-      const double* row = a.rp + (c * (int64_t)a.niter + (it - 1)) * a.D;
+      const double* row = a.rp + (c * (int64_t)a.niter + (it - 1)) * a.D + h;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        const int d = h + 4 * m;
-        p[m] = (live && d < a.D) ? row[d] : 0.0;
+        p[m] = (live && dim_ok(m)) ? row[4 * m] : 0.0;
       }
     } else {
 #pragma unroll
       for (int m = 0; m < M; m += 2) {
-        double z0, z1;
-        normal_pair(draw_block((uint32_t)(h + 4 * m), (uint32_t)it, gc, a.k0, a.k1), z0, z1);
-        const int d0 = h + 4 * m, d1 = d0 + 4;
-        if (GEN && a.pscale) {
-          z0 *= a.pscale[min(d0, a.D - 1)];
-          z1 *= a.pscale[min(d1, a.D - 1)];
+        double z0 = 0.0, z1 = 0.0;
+        if (m < mfull || (m == mfull && mrem > 0)) {   // uniform: pairs wholly in the padding are not drawn
+          normal_pair(draw_block(opaque_u32((uint32_t)(h + 4 * m)), (uint32_t)it, gc, a.k0, a.k1), z0, z1);
+          const int d0 = h + 4 * m, d1 = d0 + 4;
+          if (GEN && a.pscale) {
+            z0 *= a.pscale[min(d0, a.D - 1)];
+            z1 *= a.pscale[min(d1, a.D - 1)];
+          }
         }
-        p[m] = d0 < a.D ? z0 : 0.0;
-        p[m + 1] = d1 < a.D ? z1 : 0.0;
+        p[m] = dim_ok(m) ? z0 : 0.0;
+        p[m + 1] = dim_ok(m + 1) ? z1 : 0.0;
         if ((m & 6) == 6) __builtin_amdgcn_sched_barrier(0);   // bound the RNG chains in flight (registers)
       }
     }
@@ -111,15 +122,15 @@ __global__ __launch_bounds__(256, 1) void k_dense_iters(DenseArgs a) {
     } else {
       const uint4 r = draw_block(kDrawSlot, (uint32_t)it, gc, a.k0, a.k1);
       L = live ? uniform_int(r.x, a.L_low, a.L_high) : 0;
-      lnu = log(u53(r.z, r.w));
+      const double u = u53(r.z, r.w);
+      lnu = u > 0.0 ? fast_log(u) : -__builtin_inf();   // log(random()), :461 (ocml log keeps its
+                                                        // constants in VGPRs across the loop)
     }
     int Lmax = L;
 #pragma unroll
     for (int off = 1; off < kWave; off <<= 1) Lmax = max(Lmax, __shfl_xor(Lmax, off, kWave));
     Lmax = uniform_i(Lmax);
     // ---- leapfrog (:448 -> :831-839); chains with l >= L are frozen
-#pragma unroll
-    for (int m = 0; m < M; ++m) qi[m] = q[m];
     const bool cap = cap_wave && it <= a.n_save;
     double* capp = cap ? a.traj_q + (int64_t)(it - 1) * a.traj_stride * 2 : nullptr;
     if (cap) {   // dims 0 and 1 of chain 0 live in lanes 0 (h=0) and 16 (h=1)
@@ -181,16 +192,18 @@ __global__ __launch_bounds__(256, 1) void k_dense_iters(DenseArgs a) {
     const double E1 = 0.5 * (a.logc + chain_sum4(maha + kin));
     const double dE = E1 - E0;
     const bool accept = (dE < 0.0) || (lnu < -dE);
-    if (!accept) {
 #pragma unroll
-      for (int m = 0; m < M; ++m) q[m] = qi[m];
+    for (int m = 0; m < M; ++m) {
+      if (live && dim_ok(m)) {
+        if (accept) qh[4 * m] = q[m];
+        else q[m] = qh[4 * m];
+      }
     }
     if (live && write_row && qcb && row >= a.q_row0) {
-      double* rowp = qcb + (row % a.Lq) * a.D;
+      double* rowp = qcb + (row % a.Lq) * a.D + h;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        const int d = h + 4 * m;
-        if (d < a.D) rowp[d] = q[m];
+        if (dim_ok(m)) rowp[4 * m] = q[m];
       }
     }
     if (cap && lane == 0) {
@@ -207,11 +220,6 @@ __global__ __launch_bounds__(256, 1) void k_dense_iters(DenseArgs a) {
       n_lf += Lp;
       n_lf2 += Lp * Lp;
     }
-  }
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    const int d = h + 4 * m;
-    if (live && d < a.D) a.q[c * a.D + d] = q[m];
   }
   if (live && h == 0) a.Eprev[c] = Eprev;
   }   // tile loop
@@ -329,19 +337,26 @@ __global__ __launch_bounds__(256) void k_order_scatter(DenseArgs a, int it, bool
 }
 
 
-template <int MT, bool EXACT>
-hipError_t launch_dense_mt2(const DenseArgs& a, bool gen, bool replay, hipStream_t s) {
-  // one block per CU (the LDS copy of P limits residency to one), a few rounds of tiles each
-  const int64_t blocks = (a.ntiles + kDenseWaves - 1) / kDenseWaves;
+template <int MT, bool EXACT, int WAVES>
+void launch_dense_w(const DenseArgs& a, bool gen, bool replay, hipStream_t s) {
+  // one block per CU (the LDS copy of P limits residency to one), persistent over the tiles
+  const int64_t blocks = (a.ntiles + WAVES - 1) / WAVES;
   const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)device_cus())));
   const size_t lds = (size_t)MT * 4 * MT * kWave * sizeof(double);
   if (gen) {
-    if (replay) k_dense_iters<MT, EXACT, true, true><<<grid, 64 * kDenseWaves, lds, s>>>(a);
-    else k_dense_iters<MT, EXACT, true, false><<<grid, 64 * kDenseWaves, lds, s>>>(a);
+    if (replay) k_dense_iters<MT, EXACT, true, true, WAVES><<<grid, 64 * WAVES, lds, s>>>(a);
+    else k_dense_iters<MT, EXACT, true, false, WAVES><<<grid, 64 * WAVES, lds, s>>>(a);
   } else {
-    if (replay) k_dense_iters<MT, EXACT, false, true><<<grid, 64 * kDenseWaves, lds, s>>>(a);
-    else k_dense_iters<MT, EXACT, false, false><<<grid, 64 * kDenseWaves, lds, s>>>(a);
+    if (replay) k_dense_iters<MT, EXACT, false, true, WAVES><<<grid, 64 * WAVES, lds, s>>>(a);
+    else k_dense_iters<MT, EXACT, false, false, WAVES><<<grid, 64 * WAVES, lds, s>>>(a);
   }
+}
+
+template <int MT, bool EXACT>
+hipError_t launch_dense_mt2(const DenseArgs& a, bool gen, bool replay, hipStream_t s) {
+  // 4 waves (one per SIMD, all 512 registers): two waves per SIMD at 256 registers spill the
+  // leapfrog loop (q, p, gradient tile and P fragments need ~200 of them before addresses)
+  launch_dense_w<MT, EXACT, 4>(a, gen, replay, s);
   return hipGetLastError();
 }
 

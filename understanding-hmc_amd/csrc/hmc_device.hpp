@@ -44,6 +44,13 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1
   return c;
 }
 
+// Loop-invariant value made opaque to the optimiser at its point of use (keeps a hoisted
+// first Philox round of every draw slot from occupying registers across a whole loop).
+__device__ __forceinline__ uint32_t opaque_u32(uint32_t v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 __device__ __forceinline__ uint4 draw_block(uint32_t slot, uint32_t iter, uint64_t gchain, uint32_t k0,
                                             uint32_t k1) {
   return philox4x32_10(make_uint4(slot, iter, (uint32_t)gchain, (uint32_t)(gchain >> 32)), k0, k1);
