@@ -141,35 +141,36 @@ void k_dense_iters(DenseArgs a) {
       }
     }
     for (int l = 0; l < Lmax; ++l) {
+      // chains with l >= L are frozen by the EXEC mask of a divergent block (no per-dim selects;
+      // with L-ordered tiles the mask is nearly always full).  The MFMAs run with all lanes.
       const bool act = l < L;
+      if (act) {
 #pragma unroll
-      for (int m = 0; m < M; ++m) {
-        const int d = h + 4 * m;
-        const double dt = dim_dt<MT, GEN>(a, d);
-        const double mi = dim_minv<MT, GEN>(a, d);
-        double ph, qn;
-        if constexpr (EXACT) {
-          ph = p[m] - (dt * (mi * gval<MT>(acc, m))) * 0.5;
-          qn = q[m] + dt * ph;
-        } else {
-          ph = __builtin_fma(-0.5 * dt * mi, gval<MT>(acc, m), p[m]);
-          qn = __builtin_fma(dt, ph, q[m]);
+        for (int m = 0; m < M; ++m) {
+          const int d = h + 4 * m;
+          const double dt = dim_dt<MT, GEN>(a, d);
+          const double mi = dim_minv<MT, GEN>(a, d);
+          if constexpr (EXACT) {
+            p[m] = p[m] - (dt * (mi * gval<MT>(acc, m))) * 0.5;
+            q[m] = q[m] + dt * p[m];
+          } else {
+            p[m] = __builtin_fma(-0.5 * dt * mi, gval<MT>(acc, m), p[m]);
+            q[m] = __builtin_fma(dt, p[m], q[m]);
+          }
+          if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
-        p[m] = act ? ph : p[m];
-        q[m] = act ? qn : q[m];
-        if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
       gradient<MT, GEN>(a, sP, lane, h, q, acc);
+      if (act) {
 #pragma unroll
-      for (int m = 0; m < M; ++m) {
-        const int d = h + 4 * m;
-        const double dt = dim_dt<MT, GEN>(a, d);
-        const double mi = dim_minv<MT, GEN>(a, d);
-        double pn;
-        if constexpr (EXACT) pn = p[m] - (dt * (mi * gval<MT>(acc, m))) * 0.5;
-        else pn = __builtin_fma(-0.5 * dt * mi, gval<MT>(acc, m), p[m]);
-        p[m] = act ? pn : p[m];
-        if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        for (int m = 0; m < M; ++m) {
+          const int d = h + 4 * m;
+          const double dt = dim_dt<MT, GEN>(a, d);
+          const double mi = dim_minv<MT, GEN>(a, d);
+          if constexpr (EXACT) p[m] = p[m] - (dt * (mi * gval<MT>(acc, m))) * 0.5;
+          else p[m] = __builtin_fma(-0.5 * dt * mi, gval<MT>(acc, m), p[m]);
+          if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        }
       }
       if (cap) {
         const double q1 = __shfl(q[0], 16, kWave);
