@@ -265,33 +265,40 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
     if (!__builtin_amdgcn_ballot_w64(state != S_DONE)) break;
 
     // ================= one leapfrog for every chain inside a sub-tree (:612-614, :639)
+    // chains outside a sub-tree are frozen by the EXEC mask of a divergent block (no per-dim
+    // selects); the MFMAs and the reductions run with all lanes
     const bool act = state == S_READY;
+    if (act) {
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const int dd = h + 4 * m;
-      const double dt = dim_dt<MT, GEN>(a, dd), mi = dim_minv<MT, GEN>(a, dd);
-      double ph, qn;
-      if constexpr (EXACT) {
-        ph = p[m] - (dt * (mi * gval<MT>(acc, m))) * 0.5;
-        qn = q[m] + dt * ph;
-      } else {
-        ph = __builtin_fma(-0.5 * dt * mi, gval<MT>(acc, m), p[m]);
-        qn = __builtin_fma(dt, ph, q[m]);
+      for (int m = 0; m < M; ++m) {
+        const int dd = h + 4 * m;
+        const double dt = dim_dt<MT, GEN>(a, dd), mi = dim_minv<MT, GEN>(a, dd);
+        if constexpr (EXACT) {
+          p[m] = p[m] - (dt * (mi * gval<MT>(acc, m))) * 0.5;
+          q[m] = q[m] + dt * p[m];
+        } else {
+          p[m] = __builtin_fma(-0.5 * dt * mi, gval<MT>(acc, m), p[m]);
+          q[m] = __builtin_fma(dt, p[m], q[m]);
+        }
+        if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
-      p[m] = act ? ph : p[m];
-      q[m] = act ? qn : q[m];
-      if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
     gradient<MT, GEN>(a, sP, lane, h, q, acc);
+    if (act) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const int dd = h + 4 * m;
+        const double dt = dim_dt<MT, GEN>(a, dd), mi = dim_minv<MT, GEN>(a, dd);
+        if constexpr (EXACT) p[m] = p[m] - (dt * (mi * gval<MT>(acc, m))) * 0.5;
+        else p[m] = __builtin_fma(-0.5 * dt * mi, gval<MT>(acc, m), p[m]);
+        if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
     double mp1 = 0.0, kp1 = 0.0;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const int dd = h + 4 * m;
-      const double dt = dim_dt<MT, GEN>(a, dd), mi = dim_minv<MT, GEN>(a, dd);
-      double pn;
-      if constexpr (EXACT) pn = p[m] - (dt * (mi * gval<MT>(acc, m))) * 0.5;
-      else pn = __builtin_fma(-0.5 * dt * mi, gval<MT>(acc, m), p[m]);
-      p[m] = act ? pn : p[m];
+      const double mi = dim_minv<MT, GEN>(a, dd);
       mp1 += ((GEN && a.q0) ? q[m] - a.q0[min(dd, a.D - 1)] : q[m]) * gval<MT>(acc, m);
       kp1 += p[m] * (mi * p[m]);
       if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
