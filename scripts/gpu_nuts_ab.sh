@@ -10,7 +10,7 @@ for v in A B; do
   timeout -k 10 200 python bench.py $C --iters-per-step 2 --steps 5 --warmup 1 > gpurun_out/nab/c5_${v}_s2.log 2>&1 || exit $?
 done
 unset HMC_LIB_PATH
-for S in 8 20; do
+for S in ${NUTS_S:-}; do
   timeout -k 10 300 python bench.py $C --iters-per-step $S --steps 3 --warmup 1 > gpurun_out/nab/c5_B_s$S.log 2>&1 || exit $?
 done
 for f in gpurun_out/nab/c5_*.log; do echo $f $(grep -o '"value": [0-9.e+]*\|"lane_utilisation": [0-9.e+]*\|"ms_per_step": [0-9.e+]*' $f); done

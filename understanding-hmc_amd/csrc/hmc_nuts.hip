@@ -360,7 +360,6 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
           const double lp = udir == 0 ? -pc : p[m];
           r_dot += Dq * rp;
           l_dot += -Dq * lp;
-          if ((m & 7) == 7) __builtin_amdgcn_sched_barrier(0);
         }
       }
       r_dot = chain_sum4(r_dot);
@@ -414,7 +413,6 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         const double oq = vget<M>(W, 0, o, m), op = vget<M>(W, 1, o, m);
-        if ((m & 7) == 7) __builtin_amdgcn_sched_barrier(0);
         const double rq = udir == 0 ? q[m] : oq, lq = udir == 0 ? oq : q[m];
         const double rpp = udir == 0 ? p[m] : op, lpp = udir == 0 ? op : p[m];
         const double Dq = rq - lq;
