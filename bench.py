@@ -50,6 +50,9 @@ def parse():
                     help="no q_chain storage: R-hat/ESS from windowed streaming statistics inside the timed "
                          "loop (config 4: D=1000 at 131072 chains/GPU)")
     ap.add_argument("--tmax", type=int, default=16, help="streaming variogram lags")
+    ap.add_argument("--stream-feed", type=int, default=5,
+                    help="--stream-diag: steps between diagnostics updates (window of tmax + "
+                         "(feed+1)*iters_per_step rows; larger = less variogram carry re-reading)")
     ap.add_argument("--no-order-tiles", action="store_true",
                     help="dense targets: MFMA tiles in chain order (several iterations per launch) instead of "
                          "L-ordered tiles (one launch per iteration, chains sorted by trajectory length)")
@@ -153,7 +156,7 @@ def main():
     it = 1
     def step(i0, evs=None):
         if sd is not None:
-            eng.run_streaming(sd, i0, i0 + S, S, events=evs)
+            eng.run_streaming(sd, i0, i0 + S, S, events=evs, feed=S * a.stream_feed)
         else:
             if evs is not None:
                 evs[0].record(stream)

@@ -60,8 +60,10 @@ def _lags_needed(q):
     return out
 
 
-@pytest.mark.parametrize("thin,wu,step", [(1, 20, 10), (3, 7, 16), (2, 0, 5)])
-def test_engine_streaming_equals_stored_chain(thin, wu, step):
+@pytest.mark.parametrize("thin,wu,step,feed,per_step", [(1, 20, 10, 10, False), (3, 7, 16, 16, False),
+                                                     (2, 0, 5, 5, False), (1, 20, 10, 40, True),
+                                                     (3, 7, 8, 24, True)])
+def test_engine_streaming_equals_stored_chain(thin, wu, step, feed, per_step):
     """Same Philox run twice: whole q_chain stored vs the sliding window feeding the
     streaming statistics."""
     from hmc_amd.diagnostics import StreamingDiagnostics, convergence_stats
@@ -81,7 +83,11 @@ def test_engine_streaming_equals_stored_chain(thin, wu, step):
     R_ref, neff_ref = convergence_stats(full.q_chain[:, 1:, :], thin_rate=1, warm_up_num=0)
     st = engine(False)
     sd = StreamingDiagnostics(N, D, st.L_chain - 1, tmax=32)
-    st.run_streaming(sd, 1, Niter + 1, step)
+    if per_step:   # bench.py's pattern: one call per launch, diagnostics fed every `feed` iterations
+        for a in range(1, Niter + 1, step):
+            st.run_streaming(sd, a, min(a + step, Niter + 1), step, feed=feed)
+    else:
+        st.run_streaming(sd, 1, Niter + 1, step, feed=feed)
     R, neff = sd.finish()
     assert torch.equal(st.q, full.q)
     np.testing.assert_allclose(R, R_ref, rtol=1e-10)

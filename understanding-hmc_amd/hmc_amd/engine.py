@@ -122,16 +122,22 @@ class RandomEngine:
         H.check(H.lib().hmc_random_iters(self.T, self.K, self.schedule(it0, it1), self._replay, self.S,
                                          self.stream()), "hmc_random_iters")
 
-    def run_streaming(self, diag, it_begin, it_end, step, events=None):
+    def run_streaming(self, diag, it_begin, it_end, step, events=None, feed=None):
         """Iterations [it_begin, it_end) in launches of `step`, with q_chain rows kept only in a
         circular device window (chain row r in window row r % W) that feeds `diag`
         (diagnostics.StreamingDiagnostics): memory O(N * (tmax + step/thin) * D) instead of
         O(N * L_chain * D), no copies.  Row 0 is not a sample of the statistics (Q16); rows are
         fed once complete (a thinned row is final after its last iteration).  May be called
         repeatedly with consecutive ranges and the same `step`.
-        events: optional (start, end) CUDA events recorded around each sampler launch."""
+        events: optional (start, end) CUDA events recorded around each sampler launch.
+        feed: iterations between diagnostics updates (default `step`; a multiple of `step`).  Each
+        update re-reads the last tmax rows (variogram carry), so feeding fewer, larger windows
+        cuts the diagnostics' HBM traffic per sample from (rows + tmax + 12)/rows toward 1 row,
+        for a window of tmax + (feed + step)/thin rows.  The last iteration always flushes."""
         N, D, T = self.N, self.D, diag.tmax
-        W = T + step // self.thin + 2
+        feed = step if feed is None else int(feed)
+        assert feed >= step and feed % step == 0, "feed must be a multiple of step"
+        W = T + (feed + step) // self.thin + 2
         st = getattr(self, "_stream", None)
         if st is None or st[0] is not diag or st[1].shape[1] != W:
             st = [diag, torch.zeros((N, W, D), dtype=torch.float64, device=self.device)]
@@ -147,7 +153,7 @@ class RandomEngine:
             if events is not None:
                 events[1].record(torch.cuda.current_stream(self.device))
             done = self.L_chain if b - 1 == self.n_iter else max(0, (b - self.warm_up) // self.thin)
-            if done > next_row:
+            if done > next_row and (done - next_row >= feed // self.thin or b - 1 == self.n_iter):
                 carry = min(T, next_row - 1)
                 diag.update(win, carry, done - next_row, slot0=(next_row - carry) % W)
                 next_row = done
