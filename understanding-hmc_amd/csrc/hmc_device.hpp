@@ -306,13 +306,23 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return __hiloint2double(hi, lo);
 }
 
+// DPP move with an undefined old value: lanes a masked row leaves unwritten hold garbage.  Only
+// lane 63 is read at the end, and every step writes it, so no zero-initialising moves are needed
+// before the two row_bcast steps (4 VALU per reduction).
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ double dpp_u(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, ROW_MASK, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, ROW_MASK, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+
 __device__ __forceinline__ double wave_sum_dpp(double v) {
-  v += dpp0<0x111>(v);        // row_shr:1
-  v += dpp0<0x112>(v);        // row_shr:2
-  v += dpp0<0x114>(v);        // row_shr:4
-  v += dpp0<0x118>(v);        // row_shr:8
-  v += dpp0<0x142, 0xA>(v);   // row_bcast:15 -> rows 1, 3
-  v += dpp0<0x143, 0xC>(v);   // row_bcast:31 -> rows 2, 3
+  v += dpp_u<0x111>(v);        // row_shr:1 (bound_ctrl: lanes shifted in from outside the row read 0)
+  v += dpp_u<0x112>(v);        // row_shr:2
+  v += dpp_u<0x114>(v);        // row_shr:4
+  v += dpp_u<0x118>(v);        // row_shr:8
+  v += dpp_u<0x142, 0xA>(v);   // row_bcast:15 -> rows 1, 3
+  v += dpp_u<0x143, 0xC>(v);   // row_bcast:31 -> rows 2, 3
   return readlane_d(v, 63);
 }
 

@@ -30,7 +30,11 @@ __device__ __forceinline__ void wave_partials(const RandArgs& a, const int (&kk)
   kin = 0.0;
 #pragma unroll
   for (int j = 0; j < K; ++j) {
-    if (pv[j]) {
+    if constexpr (!GEN) {   // padding slots hold q = p = 0 (loads, draws and the integrator keep
+                            // them zero), so they add exact zeros: no masks
+      energy_terms<GEN>(DimConst{}, q[2 * j], p[2 * j], maha, kin);
+      energy_terms<GEN>(DimConst{}, q[2 * j + 1], p[2 * j + 1], maha, kin);
+    } else if (pv[j]) {
       const int d = 2 * kk[j];
       energy_terms<GEN>(dim_const<GEN>(a, d), q[2 * j], p[2 * j], maha, kin);
       if (d + 1 < a.D) energy_terms<GEN>(dim_const<GEN>(a, d + 1), q[2 * j + 1], p[2 * j + 1], maha, kin);
@@ -44,7 +48,10 @@ __device__ __forceinline__ double kin_partial(const RandArgs& a, const int (&kk)
   double kin = 0.0;
 #pragma unroll
   for (int j = 0; j < K; ++j) {
-    if (pv[j]) {
+    if constexpr (!GEN) {   // zero padding slots, as in wave_partials
+      kin += p[2 * j] * p[2 * j];
+      kin += p[2 * j + 1] * p[2 * j + 1];
+    } else if (pv[j]) {
       const int d = 2 * kk[j];
       const DimConst c0 = dim_const<GEN>(a, d);
       kin += GEN ? p[2 * j] * (c0.minv * p[2 * j]) : p[2 * j] * p[2 * j];
@@ -122,9 +129,8 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     k0 = wave_sum_dpp(k0);
   } else {                 // one reduction of V + K
     k0 = wave_sum_dpp(m0 + k0);
-    m0 = 0.0;
   }
-  double E0 = 0.5 * (a.logc + (m0 + k0));
+  double E0 = EXACT ? 0.5 * (a.logc + (m0 + k0)) : 0.5 * (a.logc + k0);
 
   // thinning bookkeeping without divisions: row = (it - wu)//thin, phase = (it - wu) % thin
   int row = 0, phase = 0;
@@ -287,9 +293,8 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
       kn = wave_sum_dpp(kn);
     } else {
       k1 = wave_sum_dpp(m1 + k1);
-      m1 = 0.0;
     }
-    const double E1 = 0.5 * (a.logc + (m1 + k1));
+    const double E1 = EXACT ? 0.5 * (a.logc + (m1 + k1)) : 0.5 * (a.logc + k1);
     const double dE = E1 - E0;                            // samplers.py:459
     const bool accept = (dE < 0.0) || (lnu < -dE);        // :462
     if (!accept && !(FULL && (a.dbg & 128))) {
