@@ -204,7 +204,7 @@ void k_dense_iters(DenseArgs a) {
       double* rowp = qcb + (row % a.Lq) * a.D + h;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        if (dim_ok(m)) rowp[4 * m] = q[m];
+        if (dim_ok(m)) __builtin_nontemporal_store(q[m], rowp + 4 * m);   // sample row: written once
       }
     }
     if (cap && lane == 0) {

@@ -290,6 +290,19 @@ __device__ __forceinline__ void store_pair(double* __restrict__ row, int k, bool
   }
 }
 
+// Same as store_pair with non-temporal stores (q_chain sample rows: written once, read back only
+// by the diagnostics after the run, so they should not displace cached lines).
+__device__ __forceinline__ void store_pair_nt(double* __restrict__ row, int k, bool even, bool v1, double a,
+                                              double b) {
+  if (even) {
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store(d2v{a, b}, reinterpret_cast<d2v*>(row + 2 * k));
+  } else {
+    __builtin_nontemporal_store(a, row + 2 * k);
+    if (v1) __builtin_nontemporal_store(b, row + 2 * k + 1);
+  }
+}
+
 // ---- full-wave fp64 sum with DPP (no LDS traffic): row_shr 1/2/4/8 prefix inside each
 // 16-lane row, then row_bcast15 / row_bcast31 fold the rows; lane 63 holds the total, which
 // v_readlane turns into a wave-uniform (SGPR) value.  EXEC must be all ones at the call.

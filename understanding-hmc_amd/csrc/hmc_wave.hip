@@ -305,7 +305,7 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
       double* rowp = qcb + (int64_t)qslot * a.D;
 #pragma unroll
       for (int j = 0; j < K; ++j)
-        if (pv[j]) store_pair(rowp, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);
+        if (pv[j]) store_pair_nt(rowp, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);
     }
     if (cap && lane == 0) {
       a.traj_len[it - 1] = (L > 0 ? L : 0) + 1;
