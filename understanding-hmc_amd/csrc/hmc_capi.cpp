@@ -144,7 +144,9 @@ const char* hmc_last_error(void) { return g_err.c_str(); }
 hmc_status hmc_chain_init(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, const hmc_replay* r,
                           const double* q_start, hmc_state* st, void* stream) {
   if (hmc_status e = check_schedule(t, k, s, false)) return e;
-  if (!st || !st->q || !st->E_prev || !q_start) return fail(HMC_EINVAL, "null state/q_start");
+  if (!st) return fail(HMC_EINVAL, "null state");
+  if (s->n_chains == 0) return HMC_OK;   // empty batch: zero-size buffers may be NULL
+  if (!st->q || !st->E_prev || !q_start) return fail(HMC_EINVAL, "null state/q_start");
   const bool replay = s->rng_mode == HMC_RNG_REPLAY;
   if (replay && (!r || !r->p0)) return fail(HMC_EINVAL, "replay mode needs p0");
   if (s->n_chains == 0) return HMC_OK;
@@ -167,12 +169,14 @@ hmc_status hmc_chain_init(const hmc_target* t, const hmc_kinetic* k, const hmc_s
 hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, const hmc_replay* r,
                             hmc_state* st, void* stream) {
   if (hmc_status e = check_schedule(t, k, s, true)) return e;
-  if (!st || !st->q || !st->E_prev) return fail(HMC_EINVAL, "null state");
+  if (!st) return fail(HMC_EINVAL, "null state");
   if (st->qc_rows < 0 || st->qc_row0 < 0) return fail(HMC_EINVAL, "qc_rows, qc_row0 must be >= 0");
   if ((st->qc_rows > 0 ? st->qc_rows : (int64_t)s->L_chain) * t->D * 8 > 0x7FFFFFFFll)
     return fail(HMC_ENOTSUP, "one chain's q_chain rows exceed 2 GiB (use a streaming window)");
   if (s->iter_begin < 1 || s->iter_end < s->iter_begin || s->iter_end > s->n_iter + 1)
     return fail(HMC_EINVAL, "iteration range must satisfy 1 <= begin <= end <= Niter+1");
+  if (s->n_chains == 0) return HMC_OK;   // empty batch: zero-size buffers may be NULL
+  if (!st->q || !st->E_prev) return fail(HMC_EINVAL, "null state");
   const bool replay = s->rng_mode == HMC_RNG_REPLAY;
   if (replay && (!r || !r->p || !r->L || !r->lnu)) return fail(HMC_EINVAL, "replay mode needs p, L, lnu");
   if (s->n_chains == 0 || s->iter_end == s->iter_begin) return HMC_OK;
@@ -232,9 +236,11 @@ int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max) {
 hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, const hmc_replay* r,
                           hmc_state* st, void* workspace, void* stream) {
   if (hmc_status e = check_schedule(t, k, s, false)) return e;
-  if (!st || !st->q || !st->E_prev) return fail(HMC_EINVAL, "null state");
+  if (!st) return fail(HMC_EINVAL, "null state");
   if (s->iter_begin < 1 || s->iter_end < s->iter_begin || s->iter_end > s->n_iter + 1)
     return fail(HMC_EINVAL, "iteration range must satisfy 1 <= begin <= end <= Niter+1");
+  if (s->n_chains == 0) return HMC_OK;   // empty batch: zero-size buffers may be NULL
+  if (!st->q || !st->E_prev) return fail(HMC_EINVAL, "null state");
   if (s->d_max < 1 || s->d_max > 15) return fail(HMC_EINVAL, "d_max must be in [1, 15]");
   if (t->kind != HMC_TARGET_DENSE) return fail(HMC_ENOTSUP, "NUTS runs the dense kernel: pass prec as dense");
   if (!hmc::dense_tiles(t->D)) return fail(HMC_ENOTSUP, "dense target: D=%d > 128 not supported", t->D);
