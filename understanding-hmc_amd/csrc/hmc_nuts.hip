@@ -15,6 +15,8 @@
 // in a workspace in HBM (`ws`, hmc_nuts_workspace_size), chain-contiguous and zero padded so
 // lanes never branch on the dimension and chains that sit out a branch move no bytes.  The tail of the workspace holds the per-chain replay-tape cursors (zeroed by the
 // host before the first launch of a run).  All cross-lane reductions run in converged control flow.
+#include <algorithm>
+
 #include "hmc_dense_ops.hpp"
 #include "hmc_device.hpp"
 #include "hmc_internal.hpp"
@@ -25,7 +27,9 @@ namespace {
 
 constexpr int kMaxDepth = 16;   // table size bound (d_max <= 15)
 
-enum : int { S_ITER_START = 0, S_SUB_START = 1, S_READY = 2, S_ITER_END = 3, S_DONE = 4 };
+// S_FETCH: the chain slot takes the next chain of the launch from the queue (or retires);
+// S_GRAD: a fetched chain waits one wave step for the MFMA gradient at its start point.
+enum : int { S_ITER_START = 0, S_SUB_START = 1, S_READY = 2, S_ITER_END = 3, S_DONE = 4, S_FETCH = 5, S_GRAD = 6 };
 
 // workspace vector ids (per chain)
 enum : int { V_OLD_Q = 0, V_OLD_G = 1, V_NEW_Q = 2, V_NEW_G = 3, V_LEFT_Q = 4, V_LEFT_P = 5, V_LEFT_G = 6,
@@ -127,32 +131,32 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
 
   const int lane = threadIdx.x & (kWave - 1);
   const int h = lane >> 4;
+  // Persistent waves with a chain queue: each of the 16 chain slots of a wave takes chains from a
+  // launch-wide counter and, when a chain has done its iterations, writes it back and takes the
+  // next one.  Slots no longer idle while the slowest tree of a fixed 16-chain group finishes
+  // (lane utilisation).  Draws are keyed by the chain, so results do not depend on which slot or
+  // wave runs it.  The tree vectors are per slot (W), the tape cursors per chain.
   const int64_t wv = (int64_t)blockIdx.x * kDenseWaves + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const int64_t c = wv * 16 + (lane & 15);
-  const bool live = c < a.n;
-  const uint64_t gc = (uint64_t)(a.chain_offset + c);
   const int64_t wave_doubles = (int64_t)nuts_nvec(a.d_max) * M * kWave;
   const int64_t n_waves = (a.n + 15) / 16;
   const WaveWS W{__builtin_amdgcn_make_buffer_rsrc(a.ws + wv * wave_doubles, 0, (int)(wave_doubles * 8), 0x00020000),
                  (lane & 15) * nuts_nvec(a.d_max) * (4 * M * 8) + h * 8};
   int64_t* const tcur = reinterpret_cast<int64_t*>(a.ws + n_waves * wave_doubles);
+  unsigned long long* const queue = reinterpret_cast<unsigned long long*>(tcur + n_waves * 16);   // zeroed per launch
+  int64_t c = 0;
+  bool live = false;
+  uint64_t gc = 0;
 
   double q[M], p[M];
   d4 acc[MT];
 #pragma unroll
-  for (int m = 0; m < M; ++m) {
-    const int d = h + 4 * m;
-    q[m] = (live && d < a.D) ? a.q[c * a.D + d] : 0.0;
-  }
-  double Eprev = live ? a.Eprev[c] : 0.0;
-  // gradient and potential at the starting point
-  gradient<MT, GEN>(a, sP, lane, h, q, acc);
-  double mp = 0.0;
+  for (int m = 0; m < M; ++m) q[m] = p[m] = 0.0;
 #pragma unroll
-  for (int m = 0; m < M; ++m) mp += ((GEN && a.q0) ? q[m] - a.q0[min(h + 4 * m, a.D - 1)] : q[m]) * gval<MT>(acc, m);
-  double maha_old = chain_sum4(mp), maha_new = 0.0;    // x.g of live_old / live_new points
+  for (int nt = 0; nt < MT; ++nt) acc[nt] = d4{0.0, 0.0, 0.0, 0.0};
+  double Eprev = 0.0;
+  double maha_old = 0.0, maha_new = 0.0;    // x.g of live_old / live_new points
 
-  int state = (live && a.it0 < a.it1) ? S_ITER_START : S_DONE;
+  int state = (a.it0 < a.it1 && wv < n_waves) ? S_FETCH : S_DONE;   // workspace has n_waves slot blocks
   int it = a.it0;
   int d = 0, k = 0, Lsub = 1, udir = 0, ndraw = 0;
   bool lterm = false, rterm = false;
@@ -160,7 +164,7 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
   // save_index_table (:535) of this chain in LDS after P; the chain's 4 lanes keep identical copies
   int* const table = reinterpret_cast<int*>(sP + MT * 4 * MT * kWave) +
                      ((threadIdx.x / kWave) * 16 + (lane & 15)) * kMaxDepth;
-  int64_t tpos = (REPLAY && live) ? tcur[c] : 0;        // replay tape cursor (persists across launches)
+  int64_t tpos = 0;                                     // replay tape cursor (persists across launches)
   unsigned long long n_lf = 0, n_unst = 0, n_dmax = 0, n_tape = 0, n_steps = 0;
 
   auto draw = [&](bool direction) -> double {           // next random number of this chain (reference order)
@@ -193,7 +197,40 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
         }
         Eprev = E_init;
         ++it;
-        state = it < a.it1 ? S_ITER_START : S_DONE;
+        state = it < a.it1 ? S_ITER_START : S_FETCH;
+      }
+      if (state == S_FETCH && live) {                   // chain done: write back its state
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          const int dd = h + 4 * m;
+          if (dd < a.D) a.q[c * a.D + dd] = q[m];
+        }
+        if (h == 0) a.Eprev[c] = Eprev;
+        if (REPLAY && h == 0) tcur[c] = tpos;
+        live = false;
+      }
+      {                                                 // next chain from the queue (converged shuffle)
+        const bool fetching = state == S_FETCH;
+        long long nc = (fetching && h == 0) ? (long long)atomicAdd(queue, 1ull) : 0ll;
+        nc = __shfl(nc, lane & 15, kWave);
+        if (fetching) {
+          if (nc < a.n) {
+            c = nc;
+            live = true;
+            gc = (uint64_t)(a.chain_offset + c);
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+              const int dd = h + 4 * m;
+              q[m] = dd < a.D ? a.q[c * a.D + dd] : 0.0;
+            }
+            Eprev = a.Eprev[c];
+            tpos = REPLAY ? tcur[c] : 0;
+            it = a.it0;
+            state = S_GRAD;                             // gradient at q in the next wave step
+          } else {
+            state = S_DONE;
+          }
+        }
       }
       const bool starting = state == S_ITER_START;
       double kin = 0.0;
@@ -305,6 +342,10 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
     }
     const double maha_pt = chain_sum4(mp1);
     const double E_tmp = 0.5 * (a.logc + (maha_pt + chain_sum4(kp1)));   // E (:618 / :643)
+    if (state == S_GRAD) {                              // fetched chain: acc = gradient at its q
+      maha_old = maha_pt;
+      state = S_ITER_START;
+    }
     if (act && h == 0) ++n_lf;
     ++n_steps;
 
@@ -437,18 +478,11 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
     }
   }
 
-  // write back chain state and counters
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    const int dd = h + 4 * m;
-    if (live && dd < a.D) a.q[c * a.D + dd] = q[m];
-  }
-  if (live && h == 0) a.Eprev[c] = Eprev;
-  if (REPLAY && live && h == 0) tcur[c] = tpos;
+  // counters (every chain's state was written back when its slot fetched the next one)
   n_lf = wave_sum_u64(n_lf);
   n_unst = wave_sum_u64(n_unst);
-  n_dmax = wave_sum_u64(live && h == 0 ? n_dmax : 0ull);
-  n_tape = wave_sum_u64(live && h == 0 ? n_tape : 0ull);
+  n_dmax = wave_sum_u64(h == 0 ? n_dmax : 0ull);
+  n_tape = wave_sum_u64(h == 0 ? n_tape : 0ull);
   if (lane == 0 && a.cnt) {
     unsigned long long* cs = a.cnt + (wv & (HMC_COUNTER_SLOTS - 1)) * HMC_NCOUNTERS;
     if (n_lf) {
@@ -464,7 +498,13 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
 
 template <int MT, bool EXACT>
 hipError_t launch_nuts_mt2(const RandArgs& a, bool gen, bool replay, hipStream_t s) {
-  const dim3 grid((unsigned)((a.n + 16 * kDenseWaves - 1) / (16 * kDenseWaves)));
+  // persistent: one block per CU (LDS: P + index tables), chains handed out by the queue
+  const int64_t blocks = (a.n + 16 * kDenseWaves - 1) / (16 * kDenseWaves);
+  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)device_cus())));
+  const int64_t n_waves = (a.n + 15) / 16;
+  const int64_t wave_doubles = (int64_t)(V_SLOTS + 2 * (a.d_max + 1)) * 4 * MT * kWave;
+  double* queue = a.ws + n_waves * wave_doubles + n_waves * 16;
+  if (hipError_t e = hipMemsetAsync(queue, 0, sizeof(unsigned long long), s)) return e;
   const size_t lds = (size_t)MT * 4 * MT * kWave * sizeof(double) + kDenseWaves * 16 * kMaxDepth * sizeof(int);
   if (gen) {
     if (replay) k_nuts_iters<MT, EXACT, true, true><<<grid, 64 * kDenseWaves, lds, s>>>(a);
@@ -486,7 +526,7 @@ hipError_t launch_nuts_mt(const RandArgs& a, bool exact, bool gen, bool replay, 
 int64_t nuts_ws_doubles(int64_t n, int D, int d_max) {
   const int MT = dense_tiles(D);
   const int64_t waves = (n + 15) / 16;
-  return waves * (int64_t)(V_SLOTS + 2 * (d_max + 1)) * 4 * MT * kWave + waves * 16;   // vectors + tape cursors
+  return waves * (int64_t)(V_SLOTS + 2 * (d_max + 1)) * 4 * MT * kWave + waves * 16 + 1;   // vectors + tape cursors + chain queue
 }
 
 hipError_t launch_nuts_iters(const RandArgs& a, bool exact, bool replay, hipStream_t s) {
