@@ -37,42 +37,63 @@ enum : int { V_OLD_Q = 0, V_OLD_G = 1, V_NEW_Q = 2, V_NEW_G = 3, V_LEFT_Q = 4, V
 
 __device__ __forceinline__ int nuts_nvec(int d_max) { return V_SLOTS + 2 * (d_max + 1); }
 
-// Workspace: per chain, nvec vectors of Dp = 4M doubles (dims, zero padded), chain-contiguous,
-// 16 chains of a wave in one block addressed through a wave-uniform buffer descriptor (SGPR base,
-// 32-bit lane offset: no 64-bit addresses kept live).  Lane (c, h) touches dims h + 4m, so one
-// chain's part of an access is 32 contiguous bytes: lanes of chains that sit out a branch cost
-// no memory traffic (a wave-linear layout would fetch whole lines for every masked access).
-// `vl` is a per-lane extra vector index (the save slot of this chain), 0 for fixed vectors.
+// Workspace: per chain slot, nvec vectors of Dp = 4M doubles (dims, zero padded), slot-contiguous,
+// the 16 slots of a wave in one block addressed through a wave-uniform buffer descriptor (SGPR
+// base, 32-bit lane offset: no 64-bit addresses kept live).  Inside a vector, lane (c, h) keeps
+// its dims h + 4m in pairs (m, m+1) at byte (m/2)*64 + h*16: one chain's part of an access is
+// 64 contiguous bytes moved by 16-byte lane accesses (half the instructions and twice the
+// contiguous span of an 8-byte-per-lane layout).  Lanes of chains that sit out a branch move
+// no bytes.  `vl` is a per-lane extra vector index (the save slot of this chain), 0 for fixed
+// vectors.
 struct WaveWS {
   __amdgpu_buffer_rsrc_t r;
-  int lane_off;   // (lane & 15) * nvec * Dp * 8 + h * 8
+  int lane_off;   // (lane & 15) * nvec * Dp * 8 + h * 16
 };
+
+__device__ __forceinline__ constexpr int ws_elem(int m) { return (m >> 1) * 64 + (m & 1) * 8; }
+
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 template <int M>
 __device__ __forceinline__ void vstore(const WaveWS& w, int v, int vl, const double (&x)[M]) {
   const int vo = w.lane_off + vl * (4 * M * 8);
 #pragma unroll
-  for (int m = 0; m < M; ++m)
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, x[m]), w.r,
-                                          vo, v * (4 * M * 8) + m * 32, 0);
+  for (int m = 0; m < M; m += 2) {
+    const u32x2 lo = __builtin_bit_cast(u32x2, x[m]), hi = __builtin_bit_cast(u32x2, x[m + 1]);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo.x, lo.y, hi.x, hi.y}, w.r, vo, v * (4 * M * 8) + ws_elem(m), 0);
+  }
 }
 
 template <int M>
 __device__ __forceinline__ void vput(const WaveWS& w, int v, int m, double x) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, x), w.r,
-                                        w.lane_off, v * (4 * M * 8) + m * 32, 0);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, x), w.r, w.lane_off, v * (4 * M * 8) + ws_elem(m), 0);
 }
 
 template <int M>
 __device__ __forceinline__ double vget(const WaveWS& w, int v, int vl, int m) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(w.r, w.lane_off + vl * (4 * M * 8),
-                                                                         v * (4 * M * 8) + m * 32, 0));
+                                                                         v * (4 * M * 8) + ws_elem(m), 0));
+}
+
+template <int M>
+__device__ __forceinline__ void vput2(const WaveWS& w, int v, int m, double x0, double x1) {
+  const u32x2 lo = __builtin_bit_cast(u32x2, x0), hi = __builtin_bit_cast(u32x2, x1);
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo.x, lo.y, hi.x, hi.y}, w.r, w.lane_off, v * (4 * M * 8) + ws_elem(m), 0);
+}
+
+// dims m and m+1 (m even) in one 16-byte access
+template <int M>
+__device__ __forceinline__ void vget2(const WaveWS& w, int v, int vl, int m, double& x0, double& x1) {
+  const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(w.r, w.lane_off + vl * (4 * M * 8), v * (4 * M * 8) + ws_elem(m), 0);
+  x0 = __builtin_bit_cast(double, u32x2{r.x, r.y});
+  x1 = __builtin_bit_cast(double, u32x2{r.z, r.w});
 }
 
 template <int M>
 __device__ __forceinline__ void vload(const WaveWS& w, int v, int vl, double (&x)[M]) {
 #pragma unroll
-  for (int m = 0; m < M; ++m) x[m] = vget<M>(w, v, vl, m);
+  for (int m = 0; m < M; m += 2) vget2<M>(w, v, vl, m, x[m], x[m + 1]);
 }
 
 template <int MT>
@@ -86,7 +107,12 @@ __device__ __forceinline__ void gstore(const WaveWS& w, int v, int vl, const d4 
 template <int MT>
 __device__ __forceinline__ void gload(const WaveWS& w, int v, int vl, d4 (&acc)[MT]) {
 #pragma unroll
-  for (int m = 0; m < 4 * MT; ++m) acc[m >> 2][m & 3] = vget<4 * MT>(w, v, vl, m);
+  for (int m = 0; m < 4 * MT; m += 2) {
+    double x0, x1;
+    vget2<4 * MT>(w, v, vl, m, x0, x1);
+    acc[m >> 2][m & 3] = x0;
+    acc[m >> 2][(m & 3) + 1] = x1;
+  }
 }
 
 // closed forms of utils.py check_points / release_fast (integer bit logic)
@@ -140,7 +166,7 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
   const int64_t wave_doubles = (int64_t)nuts_nvec(a.d_max) * M * kWave;
   const int64_t n_waves = (a.n + 15) / 16;
   const WaveWS W{__builtin_amdgcn_make_buffer_rsrc(a.ws + wv * wave_doubles, 0, (int)(wave_doubles * 8), 0x00020000),
-                 (lane & 15) * nuts_nvec(a.d_max) * (4 * M * 8) + h * 8};
+                 (lane & 15) * nuts_nvec(a.d_max) * (4 * M * 8) + h * 16};
   int64_t* const tcur = reinterpret_cast<int64_t*>(a.ws + n_waves * wave_doubles);
   unsigned long long* const queue = reinterpret_cast<unsigned long long*>(tcur + n_waves * 16);   // zeroed per launch
   int64_t c = 0;
@@ -258,10 +284,8 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
             z1 = d1 < a.D ? z1 : 0.0;
             kin += z0 * (dim_minv<MT, GEN>(a, d0) * z0);
             kin += z1 * (dim_minv<MT, GEN>(a, d1) * z1);
-            vput<M>(W, V_RIGHT_P, m, z0);
-            vput<M>(W, V_LEFT_P, m, -z0);
-            vput<M>(W, V_RIGHT_P, m + 1, z1);
-            vput<M>(W, V_LEFT_P, m + 1, -z1);
+            vput2<M>(W, V_RIGHT_P, m, z0, z1);
+            vput2<M>(W, V_LEFT_P, m, -z0, -z1);
             __builtin_amdgcn_sched_barrier(0);
           }
         }
@@ -392,10 +416,13 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
         while (s < a.d_max && table[s] != l) ++s;       // retrieve_save_index (unique match)
       double r_dot = 0.0, l_dot = 0.0;
       if (doit) {
+        double qcv[M], pcv[M];
+        vload<M>(W, V_SLOTS, 2 * s, qcv);
+        vload<M>(W, V_SLOTS + 1, 2 * s, pcv);
 #pragma unroll
         for (int m = 0; m < M; ++m) {
           // forward: left = (q_check, -p_check), right = (q, p); backward: left = (q, p), right = (q_check, -p_check)
-          const double qc = vget<M>(W, V_SLOTS, 2 * s, m), pc = vget<M>(W, V_SLOTS + 1, 2 * s, m);
+          const double qc = qcv[m], pc = pcv[m];
           const double Dq = udir == 0 ? q[m] - qc : qc - q[m];
           const double rp = udir == 0 ? p[m] : -pc;
           const double lp = udir == 0 ? -pc : p[m];
@@ -451,9 +478,12 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
         maha_old = maha_new;
       }
       const int o = udir == 0 ? V_LEFT_Q : V_RIGHT_Q;   // the other end
+      double oqv[M], opv[M];
+      vload<M>(W, 0, o, oqv);
+      vload<M>(W, 1, o, opv);
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        const double oq = vget<M>(W, 0, o, m), op = vget<M>(W, 1, o, m);
+        const double oq = oqv[m], op = opv[m];
         const double rq = udir == 0 ? q[m] : oq, lq = udir == 0 ? oq : q[m];
         const double rpp = udir == 0 ? p[m] : op, lpp = udir == 0 ? op : p[m];
         const double Dq = rq - lq;
