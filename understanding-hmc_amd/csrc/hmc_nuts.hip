@@ -130,15 +130,6 @@ __device__ __forceinline__ int cp_count(int m) {   // number of check points of 
   }
   return cnt;
 }
-__device__ __forceinline__ int cp_point(int m, int i) {   // i-th check point of even m
-  const int r = cp_r(m);
-  int pt = m - r + 1, half = r;
-  for (int j = 0; j < i; ++j) {
-    half >>= 1;
-    pt += half;
-  }
-  return pt;
-}
 __device__ __forceinline__ bool release_fast(int m, int l) {   // utils.py:367-385
   int rm = m, rl = l;
   while ((rm & (rm - 1)) != 0 && rm > 4) {
@@ -408,9 +399,16 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
     for (int off = 1; off < kWave; off <<= 1) ncheck_w = max(ncheck_w, __shfl_xor(ncheck_w, off, kWave));
     ncheck_w = uniform_i(ncheck_w);
     bool alive_chk = checking;
+    // check points of mpt, incrementally (cp_point): mpt - r + 1, then + r/2, + r/4, ...
+    int cp_half = checking ? cp_r(mpt) : 2;
+    int cp_pt = mpt - cp_half + 1;
     for (int ci = 0; ci < ncheck_w; ++ci) {
       const bool doit = alive_chk && ci < ncheck;
-      const int l = doit ? cp_point(mpt, ci) : 0;
+      if (ci > 0) {
+        cp_half >>= 1;
+        cp_pt += cp_half;
+      }
+      const int l = doit ? cp_pt : 0;
       int s = 0;
       if (doit)
         while (s < a.d_max && table[s] != l) ++s;       // retrieve_save_index (unique match)
@@ -419,16 +417,19 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
         double qcv[M], pcv[M];
         vload<M>(W, V_SLOTS, 2 * s, qcv);
         vload<M>(W, V_SLOTS + 1, 2 * s, pcv);
+        // forward: left = (q_check, -p_check), right = (q, p); backward: left = (q, p),
+        // right = (q_check, -p_check).  Both directions reduce to A = (q - qc).p and
+        // B = (q - qc).p_check (every sign flip is exact): r_dot, l_dot = (A, B) forward, (B, A)
+        // backward, term for term the reference's products.
+        double A = 0.0, B = 0.0;
 #pragma unroll
         for (int m = 0; m < M; ++m) {
-          // forward: left = (q_check, -p_check), right = (q, p); backward: left = (q, p), right = (q_check, -p_check)
-          const double qc = qcv[m], pc = pcv[m];
-          const double Dq = udir == 0 ? q[m] - qc : qc - q[m];
-          const double rp = udir == 0 ? p[m] : -pc;
-          const double lp = udir == 0 ? -pc : p[m];
-          r_dot += Dq * rp;
-          l_dot += -Dq * lp;
+          const double Dq = q[m] - qcv[m];
+          A += Dq * p[m];
+          B += Dq * pcv[m];
         }
+        r_dot = udir == 0 ? A : B;
+        l_dot = udir == 0 ? B : A;
       }
       r_dot = chain_sum4(r_dot);
       l_dot = chain_sum4(l_dot);
@@ -481,15 +482,17 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
       double oqv[M], opv[M];
       vload<M>(W, 0, o, oqv);
       vload<M>(W, 1, o, opv);
+      // A = (q - q_other).p, B = (q - q_other).p_other; (tr, tl) = (A, -B) forward, (-B, A)
+      // backward: the reference's terms up to exact sign flips
+      double tA = 0.0, tB = 0.0;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        const double oq = oqv[m], op = opv[m];
-        const double rq = udir == 0 ? q[m] : oq, lq = udir == 0 ? oq : q[m];
-        const double rpp = udir == 0 ? p[m] : op, lpp = udir == 0 ? op : p[m];
-        const double Dq = rq - lq;
-        tr += Dq * rpp;
-        tl += -Dq * lpp;
+        const double Dq = q[m] - oqv[m];
+        tA += Dq * p[m];
+        tB += Dq * opv[m];
       }
+      tr = udir == 0 ? tA : -tB;
+      tl = udir == 0 ? -tB : tA;
     }
     tr = chain_sum4(tr);
     tl = chain_sum4(tl);
