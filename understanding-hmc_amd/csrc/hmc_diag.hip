@@ -157,8 +157,10 @@ constexpr int kStreamChunk = 8;   // window rows loaded together (memory-level p
 
 // Block = 4 chain lanes x 64 dims (lane = dim: coalesced rows).  Each thread walks its chains'
 // new rows once, with the last T samples in a register ring: per element, T differences.
+// T <= 16 capped at 168 registers: three waves per SIMD keep enough rows in flight (the
+// kernel is HBM-bound; two waves per SIMD measured 10% slower).
 template <int T>
-__global__ __launch_bounds__(256) void k_stream_accum(StreamArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T <= 16 ? 3 : 1))) void k_stream_accum(StreamArgs a) {
   __shared__ double red[4][kDimTile];
   const int dl = threadIdx.x & (kDimTile - 1);
   const int rl = threadIdx.x / kDimTile;
@@ -187,6 +189,29 @@ __global__ __launch_bounds__(256) void k_stream_accum(StreamArgs a) {
         double xs[kStreamChunk];
 #pragma unroll
         for (int j = 0; j < kStreamChunk; ++j) xs[j] = (i0 + j < rows) ? at(a.carry + i0 + j) : 0.0;
+        // whole chunk inside one split half with every lag <= T available (uniform over the
+        // block): no same-half selects.  Same operations in the same order as the general path.
+        const int64_t p0 = a.pos0 + i0;
+        const int h0 = p0 >= a.n ? 1 : 0;
+        const int64_t s0 = p0 - (int64_t)h0 * a.n;
+        if (i0 + kStreamChunk <= rows && s0 >= T && s0 + kStreamChunk <= a.n) {
+#pragma unroll
+          for (int j = 0; j < kStreamChunk; ++j) {
+            const double x = xs[j];
+            const double e = x - sh[h0];
+            m1[h0] += e;
+            m2[h0] = __builtin_fma(e, e, m2[h0]);
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+              const double df = x - ring[t];
+              v[t] = __builtin_fma(df, df, v[t]);
+            }
+#pragma unroll
+            for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
+            ring[0] = x;
+          }
+          continue;
+        }
 #pragma unroll
         for (int j = 0; j < kStreamChunk; ++j) {
           if (i0 + j >= rows) break;
