@@ -5,7 +5,8 @@ on a D=100 unit-MVN target (BASELINE.json metric; configs[1] shape), fp64.
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 One step = ONE kernel launch of hmc_random_iters that advances every chain of this GPU by
---iters-per-step HMC iterations (momentum resample, L ~ U{5..19} leapfrogs, Metropolis test,
+--iters-per-step HMC iterations (auto: 40, or fewer when the stored q_chain would exceed
+--chain-budget-gb; HMC_sampler.gen_sample itself fuses a whole run into one launch) (momentum resample, L ~ U{5..19} leapfrogs, Metropolis test,
 sample stored).  Chains shard over GPUs by global chain id (Philox keyed by it): weak scaling,
 no data-path collective; RCCL is used only for the diagnostics all-reduce after timing.
 Rank 0 prints one JSON line.
@@ -34,7 +35,13 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--chains", type=int, default=131072, help="chains per GPU (8 GPUs -> 1,048,576)")
     ap.add_argument("--dim", type=int, default=100)
-    ap.add_argument("--iters-per-step", type=int, default=10)
+    ap.add_argument("--iters-per-step", type=int, default=0,
+                    help="HMC iterations fused into one launch (= one timed step); 0 = auto: 40 for the "
+                         "Random sampler (HMC_sampler.gen_sample fuses the whole run into one launch; "
+                         "shorter launches pay a per-wave start-up), lowered so the stored q_chain stays "
+                         "within --chain-budget-gb; 2 for NUTS")
+    ap.add_argument("--chain-budget-gb", type=float, default=100.0,
+                    help="HBM budget for the stored q_chain of the timed iterations (auto iters-per-step)")
     ap.add_argument("--fp-mode", default="fast", choices=["fast", "exact"])
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--dt", type=float, default=0.1)
@@ -137,6 +144,17 @@ def main():
     from hmc_amd.diagnostics import StreamingDiagnostics, convergence_stats
 
     D, N, S = a.dim, a.chains, a.iters_per_step
+    if S <= 0:
+        if a.sampler == "nuts":
+            S = 2
+        else:
+            rows = int(a.chain_budget_gb * 1e9 // (8.0 * N * D))          # q_chain rows that fit the budget
+            if a.stream_diag:     # the circular window holds tmax + (feed + 1) * S rows
+                S = 10
+            elif a.no_ess:
+                S = 40
+            else:
+                S = max(1, min(40, (rows - 1) // max(1, a.warmup + a.steps)))
     W, K = a.warmup, a.steps
     n_iter = (W + K) * S
     wu = W * S + 1                     # q_chain rows 0..K*S hold exactly the timed iterations
