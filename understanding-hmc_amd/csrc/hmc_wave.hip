@@ -366,8 +366,11 @@ __global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
   wave_iters<K, EXACT, GEN, REPLAY, FULL>(a);
 }
 
+// K = 1 blocks hold 16 waves (16 chains): the Box–Muller tables are built once per 16 chains
+// and a launch dispatches a quarter of the workgroups.
+constexpr int kK1Block = 1024;
 template <bool EXACT, bool GEN, bool REPLAY, bool FULL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_wave_iters_k1(RandArgs a) {
+__global__ __launch_bounds__(kK1Block) __attribute__((amdgpu_waves_per_eu(8))) void k_wave_iters_k1(RandArgs a) {
   wave_iters<1, EXACT, GEN, REPLAY, FULL>(a);
 }
 
@@ -375,8 +378,9 @@ template <int K, bool EXACT, bool GEN, bool REPLAY>
 void launch_wave_one(const RandArgs& a, dim3 grid, hipStream_t s) {
   const bool full = a.traj_q != nullptr || a.dbg != 0 || a.dbgL >= 0;
   if constexpr (K == 1) {
-    if (full) k_wave_iters_k1<EXACT, GEN, REPLAY, true><<<grid, 256, 0, s>>>(a);
-    else k_wave_iters_k1<EXACT, GEN, REPLAY, false><<<grid, 256, 0, s>>>(a);
+    const dim3 g1((unsigned)((a.n + kK1Block / kWave - 1) / (kK1Block / kWave)));
+    if (full) k_wave_iters_k1<EXACT, GEN, REPLAY, true><<<g1, kK1Block, 0, s>>>(a);
+    else k_wave_iters_k1<EXACT, GEN, REPLAY, false><<<g1, kK1Block, 0, s>>>(a);
   } else {
     if (full) k_wave_iters<K, EXACT, GEN, REPLAY, true><<<grid, 256, 0, s>>>(a);
     else k_wave_iters<K, EXACT, GEN, REPLAY, false><<<grid, 256, 0, s>>>(a);
