@@ -57,9 +57,10 @@ def parse():
                     help="no q_chain storage: R-hat/ESS from windowed streaming statistics inside the timed "
                          "loop (config 4: D=1000 at 131072 chains/GPU)")
     ap.add_argument("--tmax", type=int, default=16, help="streaming variogram lags")
-    ap.add_argument("--stream-feed", type=int, default=5,
+    ap.add_argument("--stream-feed", type=int, default=0,
                     help="--stream-diag: steps between diagnostics updates (window of tmax + "
-                         "(feed+1)*iters_per_step rows; larger = less variogram carry re-reading)")
+                         "(feed+1)*iters_per_step rows; larger = less variogram carry re-reading); "
+                         "0 = auto: every ~60 iterations")
     ap.add_argument("--no-order-tiles", action="store_true",
                     help="dense targets: MFMA tiles in chain order (several iterations per launch) instead of "
                          "L-ordered tiles (one launch per iteration, chains sorted by trajectory length)")
@@ -150,12 +151,13 @@ def main():
         else:
             rows = int(a.chain_budget_gb * 1e9 // (8.0 * N * D))          # q_chain rows that fit the budget
             if a.stream_diag:     # the circular window holds tmax + (feed + 1) * S rows
-                S = 10
+                S = 20
             elif a.no_ess:
                 S = 40
             else:
                 S = max(1, min(40, (rows - 1) // max(1, a.warmup + a.steps)))
     W, K = a.warmup, a.steps
+    feed_steps = a.stream_feed if a.stream_feed > 0 else max(1, 60 // S)
     n_iter = (W + K) * S
     wu = W * S + 1                     # q_chain rows 0..K*S hold exactly the timed iterations
     cov = np.eye(D) if a.rho == 0 else (np.diag(np.ones(D)) * (1 - a.rho) + a.rho)
@@ -174,7 +176,7 @@ def main():
     it = 1
     def step(i0, evs=None):
         if sd is not None:
-            eng.run_streaming(sd, i0, i0 + S, S, events=evs, feed=S * a.stream_feed)
+            eng.run_streaming(sd, i0, i0 + S, S, events=evs, feed=S * feed_steps)
         else:
             if evs is not None:
                 evs[0].record(stream)
