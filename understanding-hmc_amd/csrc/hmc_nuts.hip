@@ -140,6 +140,14 @@ __device__ __forceinline__ bool release_fast(int m, int l) {   // utils.py:367-3
   return (rm >= 4) && (rl > 1);
 }
 
+// acc + x*y: the reference's separate multiply and add in EXACT mode, one FMA in FAST mode (the
+// per-step dot products and energy sums: ~150 VALU per wave step).
+template <bool EXACT>
+__device__ __forceinline__ double mac(double acc, double x, double y) {
+  if constexpr (EXACT) return acc + x * y;
+  else return __builtin_fma(x, y, acc);
+}
+
 template <int MT, bool EXACT, bool GEN, bool REPLAY>
 __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
   constexpr int M = 4 * MT;
@@ -351,8 +359,8 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
     for (int m = 0; m < M; ++m) {
       const int dd = h + 4 * m;
       const double mi = dim_minv<MT, GEN>(a, dd);
-      mp1 += ((GEN && a.q0) ? q[m] - a.q0[min(dd, a.D - 1)] : q[m]) * gval<MT>(acc, m);
-      kp1 += p[m] * (mi * p[m]);
+      mp1 = mac<EXACT>(mp1, (GEN && a.q0) ? q[m] - a.q0[min(dd, a.D - 1)] : q[m], gval<MT>(acc, m));
+      kp1 = mac<EXACT>(kp1, p[m], mi * p[m]);
       if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
     const double maha_pt = chain_sum4(mp1);
@@ -425,8 +433,8 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
 #pragma unroll
         for (int m = 0; m < M; ++m) {
           const double Dq = q[m] - qcv[m];
-          A += Dq * p[m];
-          B += Dq * pcv[m];
+          A = mac<EXACT>(A, Dq, p[m]);
+          B = mac<EXACT>(B, Dq, pcv[m]);
         }
         r_dot = udir == 0 ? A : B;
         l_dot = udir == 0 ? B : A;
@@ -488,8 +496,8 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         const double Dq = q[m] - oqv[m];
-        tA += Dq * p[m];
-        tB += Dq * opv[m];
+        tA = mac<EXACT>(tA, Dq, p[m]);
+        tB = mac<EXACT>(tB, Dq, opv[m]);
       }
       tr = udir == 0 ? tA : -tB;
       tl = udir == 0 ? -tB : tA;
