@@ -32,6 +32,8 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVE
 void k_dense_iters(DenseArgs a) {
   constexpr int M = 4 * MT;
   extern __shared__ double sP[];
+  __shared__ double s_ntab[REPLAY ? 2 : kNormalTableDoubles];   // Box–Muller tables (Philox momentum)
+  if constexpr (!REPLAY) init_normal_tables(s_ntab);             // synchronised by stage_precision
   stage_precision<MT>(a, sP);
 
   const int lane = threadIdx.x & (kWave - 1);
@@ -82,7 +84,8 @@ void k_dense_iters(DenseArgs a) {
       for (int m = 0; m < M; m += 2) {
         double z0 = 0.0, z1 = 0.0;
         if (m < mfull || (m == mfull && mrem > 0)) {   // uniform: pairs wholly in the padding are not drawn
-          normal_pair(draw_block(opaque_u32((uint32_t)(h + 4 * m)), (uint32_t)it, gc, a.k0, a.k1), z0, z1);
+          normal_pair_tab(draw_block(opaque_u32((uint32_t)(h + 4 * m)), (uint32_t)it, gc, a.k0, a.k1), s_ntab, z0,
+                          z1);
           const int d0 = h + 4 * m, d1 = d0 + 4;
           if (GEN && a.pscale) {
             z0 *= a.pscale[min(d0, a.D - 1)];
