@@ -1,8 +1,10 @@
-"""Condense a scripts/profile.sh run into profiles/<tag>_*.{csv,json} (committed evidence).
+"""Condense a `scripts/gpu.sh prof` run into profiles/<tag>_*.{csv,json} (committed evidence).
 
-HBM bytes per launch of the hot kernel = 2 x FETCH_SIZE + WRITE_SIZE (KB -> B), the x2 being
-the gfx950 correction for wide coalesced reads (MI355X_MICROARCH.md §HBM).  The hot kernel
-reads only its state (q, E_prev) once per launch; its traffic is dominated by stores."""
+HBM bytes per launch of the hot kernel = 2 x FETCH_SIZE + WRITE_SIZE (KB -> B), the x2 being the
+gfx950 correction for wide coalesced reads (MI355X_MICROARCH.md §HBM).  Only the timed launches
+(the last `steps` dispatches of the hot kernel) are averaged.  The entry is keyed by the launch
+shape the bench line reports (roofline.shape), and bench.py attaches it to a line only when that
+line has the same shape."""
 import csv
 import glob
 import json
@@ -11,7 +13,6 @@ import shutil
 import sys
 
 out, tag = sys.argv[1], sys.argv[2]
-write_traffic_file = "--no-traffic-file" not in sys.argv[3:]
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(ROOT, "profiles")
 os.makedirs(prof, exist_ok=True)
@@ -19,15 +20,27 @@ HOT = ("k_wave_iters", "k_random_iters", "k_dense_iters", "k_nuts_iters")
 
 
 def one(pattern):
-    f = glob.glob(os.path.join(out, pattern), recursive=True)
+    f = sorted(glob.glob(os.path.join(out, pattern), recursive=True))
     return f[0] if f else None
 
 
+def bench_line(logname):
+    """The bench JSON line printed during a profiled run."""
+    try:
+        for line in open(os.path.join(out, logname)):
+            if line.startswith("{") and '"metric"' in line:
+                return json.loads(line)
+    except OSError:
+        pass
+    return None
+
+
+line = bench_line("trace.log") or bench_line("fetch.log")
+steps = line["steps"] if line else 10
+summary = {"tag": tag, "bench_line": line}
 stats = one("trace/**/run_kernel_stats.csv")
 if stats:
     shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
-summary = {"tag": tag}
-if stats:
     rows = list(csv.DictReader(open(stats)))
     hot = [r for r in rows if any(h in r["Name"] for h in HOT)]
     if hot:
@@ -37,17 +50,13 @@ if stats:
         summary["hot_calls"] = int(h["Calls"])
 
 
-def pmc(sub, name, timed_only=True):
-    """Mean of a PMC counter over the hot kernel's dispatches; the bench's warm-up launches
-    (which store no q_chain rows) are dropped by keeping the last 10 dispatches (= --steps 10)."""
+def pmc(sub, name):
     f = one(f"{sub}/**/run_counter_collection.csv")
     if not f:
         return None
     rows = [r for r in csv.DictReader(open(f)) if r["Counter_Name"] == name and any(h in r["Kernel_Name"] for h in HOT)]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    vals = [float(r["Counter_Value"]) for r in rows]
-    if timed_only and len(vals) > 10:
-        vals = vals[-10:]
+    vals = [float(r["Counter_Value"]) for r in rows][-steps:]
     return sum(vals) / len(vals) if vals else None
 
 
@@ -57,19 +66,26 @@ if fetch_kb is not None and write_kb is not None:
     summary["write_size_kb"] = write_kb
     summary["bytes_per_launch"] = (2.0 * fetch_kb + write_kb) * 1024.0
 sq = {}
-for sub in ("sq", "sq2"):
-    f = one(f"{sub}/**/run_counter_collection.csv")
-    if f:
-        agg = {}
-        for r in csv.DictReader(open(f)):
-            if any(h in r["Kernel_Name"] for h in HOT):
-                agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-        sq.update({k: sum(v) / len(v) for k, v in agg.items()})
-if sq:
+f = one("sq/**/run_counter_collection.csv")
+if f:
+    agg = {}
+    for r in csv.DictReader(open(f)):
+        if any(h in r["Kernel_Name"] for h in HOT):
+            agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    sq = {k: sum(v[-steps:]) / len(v[-steps:]) for k, v in agg.items()}
     summary["sq"] = sq
 json.dump(summary, open(os.path.join(prof, f"{tag}_profile_summary.json"), "w"), indent=1)
-if "bytes_per_launch" in summary and write_traffic_file:
-    json.dump({"bytes_per_launch": summary["bytes_per_launch"], "source": f"profiles/{tag}_profile_summary.json",
-               "kernel": summary.get("hot_kernel")},
-              open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
-print(json.dumps(summary, indent=1))
+
+shape = (line or {}).get("roofline", {}).get("shape") or (line or {}).get("memory", {}).get("shape")
+if "bytes_per_launch" in summary and shape:
+    path = os.path.join(prof, "pmc_traffic.json")
+    try:
+        entries = json.load(open(path))
+        entries = entries if isinstance(entries, list) else []
+    except (OSError, ValueError):
+        entries = []
+    entries = [e for e in entries if e.get("shape") != shape]
+    entries.append({"shape": shape, "bytes_per_launch": summary["bytes_per_launch"],
+                    "source": f"profiles/{tag}_profile_summary.json", "kernel": summary.get("hot_kernel")})
+    json.dump(entries, open(path, "w"), indent=1)
+print(json.dumps({k: v for k, v in summary.items() if k != "bench_line"}, indent=1))

@@ -15,8 +15,10 @@
 namespace {
 
 thread_local std::string g_err;
+#ifdef HMC_DEBUG_HOOKS
 unsigned long long* g_stamps = nullptr;   // HMC_DEBUG_STAMPS diagnostic buffer
 int64_t g_stamp_waves = 0;
+#endif
 
 hmc_status fail(hmc_status st, const char* fmt, ...) {
   char buf[512];
@@ -54,6 +56,16 @@ hmc_status check_schedule(const hmc_target* t, const hmc_kinetic* k, const hmc_s
   if (random && s->rng_mode == HMC_RNG_PHILOX && s->L_low < 0) return fail(HMC_EINVAL, "L_low < 0");
   if (s->rng_mode != HMC_RNG_REPLAY && s->rng_mode != HMC_RNG_PHILOX) return fail(HMC_EINVAL, "bad rng_mode");
   if (s->fp_mode != HMC_MODE_EXACT && s->fp_mode != HMC_MODE_FAST) return fail(HMC_EINVAL, "bad fp_mode");
+  return HMC_OK;
+}
+
+// q_chain buffer geometry shared by the Random and NUTS kernels: the kernels index one chain's
+// rows with 32-bit row numbers (row % Lq), so a chain's rows must stay within 2 GiB.
+hmc_status check_window(const hmc_target* t, const hmc_schedule* s, const hmc_state* st) {
+  if (st->qc_rows < 0 || st->qc_row0 < 0) return fail(HMC_EINVAL, "qc_rows, qc_row0 must be >= 0");
+  if (st->qc_rows > 0x7FFFFFFFll || st->qc_row0 > 0x7FFFFFFFll) return fail(HMC_EINVAL, "qc_rows/qc_row0 too large");
+  if ((st->qc_rows > 0 ? st->qc_rows : (int64_t)s->L_chain) * t->D * 8 > 0x7FFFFFFFll)
+    return fail(HMC_ENOTSUP, "one chain's q_chain rows exceed 2 GiB (use a streaming window)");
   return HMC_OK;
 }
 
@@ -100,8 +112,11 @@ hmc::RandArgs rand_args(const hmc_target* t, const hmc_kinetic* k, const hmc_sch
   a.Ec = st->E_chain;
   a.dEc = st->dE_chain;
   a.cnt = st->counters;
-  if (const char* ab = getenv("HMC_DEBUG_ABLATE")) a.dbg = atoi(ab);   // profiling experiments only
   a.dbgL = -1;
+#ifdef HMC_DEBUG_HOOKS
+  // Profiling experiments only: compiled into the separate debug build (make debug ->
+  // lib/libhmc_debug.so), never into the release libhmc.so the product and bench.py load.
+  if (const char* ab = getenv("HMC_DEBUG_ABLATE")) a.dbg = atoi(ab);
   if (const char* dl = getenv("HMC_DEBUG_L")) a.dbgL = atoi(dl);
   if (getenv("HMC_DEBUG_STAMPS")) {                                     // diagnostic phase timers
     const int64_t waves = (s->n_chains + lay.cpw - 1) / lay.cpw;
@@ -110,6 +125,7 @@ hmc::RandArgs rand_args(const hmc_target* t, const hmc_kinetic* k, const hmc_sch
     g_stamp_waves = waves;
     if (hipMalloc(&g_stamps, waves * 8 * sizeof(unsigned long long)) == hipSuccess) a.stamps = g_stamps;
   }
+#endif
   if (st->traj_q && st->traj_len && st->decision && st->n_save > 0) {
     a.traj_q = st->traj_q;
     a.traj_len = st->traj_len;
@@ -128,7 +144,8 @@ bool general_diag(const hmc_target* t, const hmc_kinetic* k) {
 
 extern "C" {
 
-// Diagnostic: copy the per-wave phase timers of the last HMC_DEBUG_STAMPS launch (not in hmc.h).
+#ifdef HMC_DEBUG_HOOKS
+// Diagnostic: copy the per-wave phase timers of the last HMC_DEBUG_STAMPS launch (debug build only).
 int64_t hmc_debug_stamps(unsigned long long* host, int64_t cap_words) {
   if (!g_stamps) return 0;
   const int64_t words = g_stamp_waves * 8 < cap_words ? g_stamp_waves * 8 : cap_words;
@@ -136,6 +153,7 @@ int64_t hmc_debug_stamps(unsigned long long* host, int64_t cap_words) {
   if (hipMemcpy(host, g_stamps, words * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return 0;
   return words;
 }
+#endif
 
 const char* hmc_version(void) { return "hmc_amd 0.1.0 gfx950 (diag random kernels, C ABI v1)"; }
 
@@ -170,9 +188,7 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
                             hmc_state* st, void* stream) {
   if (hmc_status e = check_schedule(t, k, s, true)) return e;
   if (!st) return fail(HMC_EINVAL, "null state");
-  if (st->qc_rows < 0 || st->qc_row0 < 0) return fail(HMC_EINVAL, "qc_rows, qc_row0 must be >= 0");
-  if ((st->qc_rows > 0 ? st->qc_rows : (int64_t)s->L_chain) * t->D * 8 > 0x7FFFFFFFll)
-    return fail(HMC_ENOTSUP, "one chain's q_chain rows exceed 2 GiB (use a streaming window)");
+  if (hmc_status e = check_window(t, s, st)) return e;
   if (s->iter_begin < 1 || s->iter_end < s->iter_begin || s->iter_end > s->n_iter + 1)
     return fail(HMC_EINVAL, "iteration range must satisfy 1 <= begin <= end <= Niter+1");
   if (s->n_chains == 0) return HMC_OK;   // empty batch: zero-size buffers may be NULL
@@ -237,6 +253,7 @@ hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_s
                           hmc_state* st, void* workspace, void* stream) {
   if (hmc_status e = check_schedule(t, k, s, false)) return e;
   if (!st) return fail(HMC_EINVAL, "null state");
+  if (hmc_status e = check_window(t, s, st)) return e;
   if (s->iter_begin < 1 || s->iter_end < s->iter_begin || s->iter_end > s->n_iter + 1)
     return fail(HMC_EINVAL, "iteration range must satisfy 1 <= begin <= end <= Niter+1");
   if (s->n_chains == 0) return HMC_OK;   // empty batch: zero-size buffers may be NULL

@@ -107,31 +107,64 @@ __global__ __launch_bounds__(256) void k_colsum_acc(const double* partial, int64
   out[c] += acc;
 }
 
-// partial[chunk][t - t0][d] = sum over split chains j of the chunk of sum_s (x_j[s+t]-x_j[s])^2.
-__global__ __launch_bounds__(256) void k_variogram_partial(Src s, int t0, int t1, int64_t jchunk, double* partial) {
+// partial[chunk][k][d] = sum over the chunk's split chains j of sum_s (x_j[s+t]-x_j[s])^2 for the lags
+// t = t0 + k, k < nt <= T.  ONE pass over the samples (round 1 re-read the chain once per lag):
+// each thread walks its chains' samples s = t0 .. n-1 with a register ring holding
+// x[s-t0], x[s-t0-1], ..., x[s-t0-T+1]; per sample it reads x[s] and the delayed x[s-t0] (the same
+// value for t0 = 1, a second, cache-friendly stream otherwise).  Lane = dim: coalesced rows.
+template <int T>
+__global__ __launch_bounds__(256) void k_variogram_ring(Src s, int t0, int nt, int64_t jchunk, double* partial) {
   __shared__ double red[4][kDimTile];
   const int dl = threadIdx.x & (kDimTile - 1);
   const int rl = threadIdx.x / kDimTile;
   const int d = blockIdx.y * kDimTile + dl;
   const int64_t j0 = (int64_t)blockIdx.x * jchunk;
   const int64_t j1 = min(j0 + jchunk, 2 * s.n_chains);
-  const int nt = t1 - t0;
-  for (int t = t0; t < t1; ++t) {
-    double acc = 0.0;
-    if (d < s.D) {
-      for (int64_t j = j0 + rl; j < j1; j += 4) {
-        const double* b = split_ptr(s, j, 0) + d;
-        for (int m = 0; m + t < s.n; ++m) {
-          const double e = b[(int64_t)(m + t) * s.sample_stride] - b[(int64_t)m * s.sample_stride];
-          acc += e * e;
+  const int64_t ss = s.sample_stride;
+  double v[T];
+#pragma unroll
+  for (int k = 0; k < T; ++k) v[k] = 0.0;
+  if (d < s.D) {
+    for (int64_t j = j0 + rl; j < j1; j += 4) {
+      const double* b = split_ptr(s, j, 0) + d;
+      double ring[T];
+#pragma unroll
+      for (int k = 0; k < T; ++k) ring[k] = 0.0;
+      int i = t0;
+      // fill: ring slot k is valid once i - t0 >= k
+      for (; i < s.n && i - t0 < T - 1; ++i) {
+#pragma unroll
+        for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
+        ring[0] = b[(int64_t)(i - t0) * ss];
+        const double x = b[(int64_t)i * ss];
+#pragma unroll
+        for (int k = 0; k < T; ++k) {
+          const double e = x - ring[k];
+          v[k] = (k <= i - t0) ? __builtin_fma(e, e, v[k]) : v[k];
+        }
+      }
+      for (; i < s.n; ++i) {
+#pragma unroll
+        for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
+        ring[0] = b[(int64_t)(i - t0) * ss];
+        const double x = b[(int64_t)i * ss];
+#pragma unroll
+        for (int k = 0; k < T; ++k) {
+          const double e = x - ring[k];
+          v[k] = __builtin_fma(e, e, v[k]);
         }
       }
     }
-    red[rl][dl] = acc;
-    __syncthreads();
-    if (rl == 0 && d < s.D)
-      partial[((int64_t)blockIdx.x * nt + (t - t0)) * s.D + d] = ((red[0][dl] + red[1][dl]) + red[2][dl]) + red[3][dl];
-    __syncthreads();
+  }
+#pragma unroll
+  for (int k = 0; k < T; ++k) {
+    if (k < nt) {
+      red[rl][dl] = v[k];
+      __syncthreads();
+      if (rl == 0 && d < s.D)
+        partial[((int64_t)blockIdx.x * nt + k) * s.D + d] = ((red[0][dl] + red[1][dl]) + red[2][dl]) + red[3][dl];
+      __syncthreads();
+    }
   }
 }
 
@@ -319,11 +352,19 @@ hipError_t launch_variogram(const double* x, int64_t n_chains, int64_t cs, int64
   const int64_t jc = vario_jchunk(m2);
   const int64_t nch = (m2 + jc - 1) / jc;
   dim3 grid((unsigned)nch, (unsigned)((D + kDimTile - 1) / kDimTile));
-  k_variogram_partial<<<grid, 256, 0, st>>>(s, t0, t1, jc, work);
-  if (hipError_t e = hipGetLastError()) return e;
-  const int64_t ncols = (int64_t)(t1 - t0) * D;
-  k_colsum_final<<<(unsigned)((ncols + 255) / 256), 256, 0, st>>>(work, nch, ncols, out);
-  return hipGetLastError();
+  // lags in blocks of <= 32 per pass; work holds [nch][t1 - t0][D] partials
+  for (int a = t0; a < t1; a += 32) {
+    const int nt = t1 - a < 32 ? t1 - a : 32;
+    double* part = work + (int64_t)nch * (a - t0) * D;
+    if (nt <= 8) k_variogram_ring<8><<<grid, 256, 0, st>>>(s, a, nt, jc, part);
+    else if (nt <= 16) k_variogram_ring<16><<<grid, 256, 0, st>>>(s, a, nt, jc, part);
+    else k_variogram_ring<32><<<grid, 256, 0, st>>>(s, a, nt, jc, part);
+    if (hipError_t e = hipGetLastError()) return e;
+    const int64_t ncols = (int64_t)nt * D;
+    k_colsum_final<<<(unsigned)((ncols + 255) / 256), 256, 0, st>>>(part, nch, ncols, out + (int64_t)(a - t0) * D);
+    if (hipError_t e = hipGetLastError()) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace hmc
