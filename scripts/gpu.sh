@@ -3,8 +3,9 @@
 #   bash scripts/gpu.sh test    TAG                 pytest -m gpu + smoke()
 #   bash scripts/gpu.sh bench   TAG [bench args]    one bench.py line -> gpurun_out/bench_TAG.json
 #   bash scripts/gpu.sh prof    TAG [bench args]    rocprofv3 kernel trace + stats, FETCH_SIZE and WRITE_SIZE
-#                                                   (separate --pmc passes), SQ counters; summarised into
-#                                                   profiles/TAG_* by scripts/summarize_profile.py
+#                                                   (separate --pmc passes), SQ counters; summarise them
+#                                                   into profiles/TAG_* afterwards, in the build container:
+#                                                   python scripts/summarize_profile.py gpurun_out/prof_TAG TAG
 #   bash scripts/gpu.sh pmc     TAG "CNT CNT ..." [bench args]   one extra --pmc pass (<= hardware limits)
 #   bash scripts/gpu.sh configs TAG                 bench lines + kernel stats of BASELINE configs 3, 4, 5
 #   bash scripts/gpu.sh round   TAG                 test, default bench, prof of the default bench
@@ -45,7 +46,6 @@ do_prof() {    # bench args...
    timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_WAVE_CYCLES \
      SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU --output-format csv -d "$OUT/sq" -o run -- \
      python3 "$R/bench.py" $ARGS > "$OUT/sq.log" 2>&1) || return $?
-  python3 scripts/summarize_profile.py "$OUT" "$TAG"
 }
 
 do_pmc() {     # "counters" bench args...
