@@ -6,7 +6,7 @@ import glob
 import sys
 
 d, kern = sys.argv[1], sys.argv[2]
-for f in sorted(glob.glob(f"{d}/p*/**/run_counter_collection.csv", recursive=True)):
+for f in sorted(glob.glob(f"{d}/**/run_counter_collection.csv", recursive=True)):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
         if kern in r["Kernel_Name"]:

@@ -38,8 +38,8 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1
                    (uint32_t)p0);
     // key schedule on the SALU at the point of use: hoisted out of the chain loop it would hold
     // 20 SGPRs and be spilled (v_readlane per round)
-    asm volatile("s_add_u32 %0, %0, 0x9E3779B9" : "+s"(k0));
-    asm volatile("s_add_u32 %0, %0, 0xBB67AE85" : "+s"(k1));
+    asm volatile("s_add_u32 %0, %0, 0x9E3779B9" : "+s"(k0) : : "scc");
+    asm volatile("s_add_u32 %0, %0, 0xBB67AE85" : "+s"(k1) : : "scc");
   }
   return c;
 }

@@ -395,12 +395,14 @@ static double expected_max(int lo, int hi, int c) {
 Layout choose_layout(int D, int L_low, int L_high) {
   static const int Ks[] = {1, 2, 4, 5, 8, 16};
   Layout best{0, 0, 0, (D + 1) / 2};
+#ifdef HMC_DEBUG_HOOKS
   if (const char* fk = getenv("HMC_FORCE_K")) {   // experiments: force the pairs-per-lane template
     const int K = atoi(fk);
     const int lpc = (best.npairs + K - 1) / K;
     for (int k : Ks)
       if (k == K && lpc <= kWave) return Layout{K, lpc, kWave / lpc, best.npairs};
   }
+#endif
   // D > 64: one wavefront per chain (hmc_wave.hip): no trajectory-length divergence inside a
   // wave, wave-uniform control flow; K pairs per lane.
   if (best.npairs > kWave / 2) {
@@ -444,9 +446,13 @@ hipError_t launch_random_init(const RandArgs& a, const Layout& lay, bool gen, bo
 
 hipError_t launch_random_iters(const RandArgs& a, const Layout& lay, bool exact, bool gen, bool replay,
                                hipStream_t s) {
+#ifdef HMC_DEBUG_HOOKS
   const char* kern = getenv("HMC_KERNEL");       // experiments: "group" forces the lane-group kernel
-  if (lay.cpw == 1 && !(kern && kern[0] == 'g') && (lay.K == 1 || lay.K == 2 || lay.K == 4 || lay.K == 8 ||
-                                                  lay.K == 16))
+  const bool force_group = kern && kern[0] == 'g';
+#else
+  const bool force_group = false;
+#endif
+  if (lay.cpw == 1 && !force_group && (lay.K == 1 || lay.K == 2 || lay.K == 4 || lay.K == 8 || lay.K == 16))
     return launch_wave_iters(a, lay.K, exact, gen, replay, s);
   const dim3 grid = grid_for(a);
   switch (lay.K) {

@@ -89,13 +89,32 @@ __device__ __forceinline__ void wave_momentum(const RandArgs& a, int64_t c, uint
   }
 }
 
+// K = 1 blocks hold 16 waves (16 chains): the Box–Muller tables are built once per 16 chains
+// and a launch dispatches a quarter of the workgroups.
+constexpr int kK1Block = 1024;
+
+// Momentum ring (K = 1, Philox): at D <= 128 a chain's npairs = ceil(D/2) coordinate pairs leave
+// 64 - npairs lanes idle (14 of 64 at D = 100), and the momentum draws (Philox4x32-10 +
+// Box–Muller, ~95 VALU per pass) are the largest part of an iteration.  The wave instead draws
+// 64 consecutive pairs per pass on ALL lanes into a per-wave LDS ring (pair g of the launch in
+// slot g % kRingPairs) and every iteration reads its npairs pairs back: npairs/64 passes per
+// iteration instead of one.  Pair k of iteration it is still keyed (k, it, chain), so every value
+// is the one the per-lane scheme draws (independent of launch splits and of the ring).
+constexpr int kRingPairs = 128;
+
 // FULL: chain-0 trajectory capture and the ablation/debug hooks compiled in.  The production
 // variant (FULL = false) drops them: their pointers and flags are live across the iteration loop
 // and pushed the SGPR demand past the 8-waves/SIMD budget (spills to VGPR lanes cost one
 // v_readlane/v_writelane VALU slot each, ~45 per iteration).
 template <int K, bool EXACT, bool GEN, bool REPLAY, bool FULL>
 __device__ __forceinline__ void wave_iters(const RandArgs& a) {
+#ifdef HMC_NO_RING
+  constexpr bool RING = false;
+#else
+  constexpr bool RING = K == 1 && !REPLAY;
+#endif
   __shared__ double s_ntab[REPLAY ? 2 : kNormalTableDoubles];   // Box–Muller tables (Philox mode)
+  __shared__ double s_ring[RING ? (kK1Block / kWave) * 2 * kRingPairs : 2];
   if constexpr (!REPLAY) {
     init_normal_tables(s_ntab);
     __syncthreads();
@@ -104,6 +123,40 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
   const int64_t c = uniform_i(blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave));
   if (c >= a.n) return;                                  // whole wave, uniform
   const uint64_t gc = (uint64_t)(a.chain_offset + c);
+  double* const ring = s_ring + (RING ? (threadIdx.x / kWave) * 2 * kRingPairs : 0);
+  int gen_n = 0, gen_it = a.it0, gen_k = 0;              // pairs drawn so far; (iteration, pair) of the next
+  // momentum of iteration `it` through the ring: at most one 64-pair pass is due (the pairs drawn
+  // so far cover every earlier iteration and npairs <= 64), and the ring never holds more than
+  // npairs + 64 <= kRingPairs pairs that are not consumed yet
+  auto ring_momentum = [&](int it, double (&pp)[2 * K]) {
+    const int base = (it - a.it0) * a.npairs;
+    if (gen_n < base + a.npairs) {                       // wave-uniform
+      int k = gen_k + lane, itl = gen_it;
+      if (k >= a.npairs) { k -= a.npairs; ++itl; }
+      if (k >= a.npairs) { k -= a.npairs; ++itl; }
+      double z0, z1;
+      normal_pair_tab(draw_block((uint32_t)k, (uint32_t)itl, gc, a.k0, a.k1), s_ntab, z0, z1);
+      *reinterpret_cast<double2*>(ring + 2 * ((gen_n + lane) & (kRingPairs - 1))) = make_double2(z0, z1);
+      __builtin_amdgcn_wave_barrier();
+      gen_n += kWave;
+      gen_k += kWave;
+      while (gen_k >= a.npairs) {
+        gen_k -= a.npairs;
+        ++gen_it;
+      }
+    }
+    pp[0] = pp[1] = 0.0;
+    if (lane < a.npairs) {
+      const double2 z = *reinterpret_cast<const double2*>(ring + 2 * ((base + lane) & (kRingPairs - 1)));
+      const int d = 2 * lane;
+      pp[0] = z.x;
+      pp[1] = d + 1 < a.D ? z.y : 0.0;
+      if (GEN && a.pscale) {
+        pp[0] *= a.pscale[d];
+        if (d + 1 < a.D) pp[1] *= a.pscale[d + 1];
+      }
+    }
+  };
   const bool even = (a.D & 1) == 0;
   int kk[K];
   bool pv[K];
@@ -120,7 +173,8 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
   __builtin_amdgcn_s_waitcnt(0x0F70);                    // retire state loads before the loop (vmcnt(0))
 
   // momentum and energy of the first iteration of this launch
-  wave_momentum<K, GEN, REPLAY>(a, c, gc, a.it0, kk, pv, p, s_ntab);
+  if constexpr (RING) ring_momentum(a.it0, p);
+  else wave_momentum<K, GEN, REPLAY>(a, c, gc, a.it0, kk, pv, p, s_ntab);
   double m0, k0, m0l;   // m0l: this lane's part of the potential of q (FAST mode bookkeeping)
   wave_partials<K, GEN>(a, kk, pv, q, p, m0, k0);
   m0l = m0;
@@ -281,7 +335,8 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     const bool more = it + 1 < a.it1;
     double kn = 0.0;
     if (more && !(FULL && (a.dbg & 256))) {
-      wave_momentum<K, GEN, REPLAY>(a, c, gc, it + 1, kk, pv, pn, s_ntab);
+      if constexpr (RING) ring_momentum(it + 1, pn);
+      else wave_momentum<K, GEN, REPLAY>(a, c, gc, it + 1, kk, pv, pn, s_ntab);
       kn = kin_partial<K, GEN>(a, kk, pv, pn);
     }
     double m1, k1, m1l;
@@ -366,9 +421,6 @@ __global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
   wave_iters<K, EXACT, GEN, REPLAY, FULL>(a);
 }
 
-// K = 1 blocks hold 16 waves (16 chains): the Box–Muller tables are built once per 16 chains
-// and a launch dispatches a quarter of the workgroups.
-constexpr int kK1Block = 1024;
 template <bool EXACT, bool GEN, bool REPLAY, bool FULL>
 __global__ __launch_bounds__(kK1Block) __attribute__((amdgpu_waves_per_eu(8))) void k_wave_iters_k1(RandArgs a) {
   wave_iters<1, EXACT, GEN, REPLAY, FULL>(a);
