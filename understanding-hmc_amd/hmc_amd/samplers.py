@@ -64,10 +64,13 @@ class sampler(object):
         self.R_q, self.n_eff_q = U.convergence_stats(src[:, 1:, :], warm_up_num=0, thin_rate=1)
         return
 
-    def plot_samples(self, *args, **kwargs):
-        """Host-side matplotlib summary figure (samplers.py:67-291) — out of scope of the
-        accelerated path: not provided by this build."""
-        raise NotImplementedError("plot_samples is host visualisation, outside the accelerated path")
+    def plot_samples(self, title_prefix, show=False, savefig=False, xmax=None, dx=None, plot_normal=True,
+                     plot_cov=True, q0=None, cov0=None):
+        """samplers.py:67-291: the 3x3 summary figure, drawn on the host from the GPU results
+        (hmc_amd.plots).  Returns the figure's numbers (plots.sample_summary)."""
+        from . import plots
+        return plots.plot_samples(self, title_prefix, show=show, savefig=savefig, xmax=xmax, dx=dx,
+                                  plot_normal=plot_normal, plot_cov=plot_cov, q0=q0, cov0=cov0)
 
 
 class HMC_sampler(sampler):
@@ -358,6 +361,14 @@ class HMC_sampler(sampler):
         """samplers.py:825-829 (host draw from the global legacy RNG, as the reference)."""
         return np.random.multivariate_normal(np.zeros(self.D), self.cov_p, size=1)
 
-    def make_movie(self, *args, **kwargs):
-        """PNG slide deck (samplers.py:843-924): host visualisation, out of scope."""
-        raise NotImplementedError("make_movie is host visualisation, outside the accelerated path")
+    def make_movie(self, title_prefix, q0=None, cov0=None, plot_cov=True, qmin=-3, qmax=3, **kwargs):
+        """samplers.py:843-880: PNG deck of chain 0's captured trajectories (hmc_amd.plots)."""
+        from . import plots
+        return plots.make_movie(self, title_prefix, q0=q0, cov0=cov0, plot_cov=plot_cov, qmin=qmin, qmax=qmax,
+                                **kwargs)
+
+    def make_slide(self, title_prefix, idx, phi_q, q_accepted, decision, q0=None, cov0=None, plot_cov=False,
+                   qmin=-3, qmax=3):
+        """samplers.py:883-924."""
+        from . import plots
+        return plots.make_slide(title_prefix, idx, phi_q, q_accepted, decision, q0, cov0, plot_cov, qmin, qmax)
