@@ -129,3 +129,61 @@ def test_checkpoint_resume_bitexact(tmp_path):
     np.testing.assert_array_equal(b.read_counters(), ref.read_counters())
     np.testing.assert_array_equal(R, R_ref)
     np.testing.assert_array_equal(neff, neff_ref)
+
+
+@pytest.mark.parametrize("sampler_type", ["Random", "NUTS"])
+def test_sampler_streaming_mode_matches_oracle(sampler_type):
+    """HMC_sampler(store_chain=False): the surface's streaming mode (samplers.py:53-64 ->
+    utils.py:77-179 without a q_chain).  Replay-mode Random chains are bit-identical to the
+    oracle's, so R-hat must equal the oracle's convergence_stats on the oracle's q_chain to
+    1e-10 rel and ESS likewise wherever the reference reads no lag beyond stream_tmax."""
+    from hmc_amd.samplers import HMC_sampler
+    D, N, Niter, wu = 10, 24, 300, 60
+    tgt = O.MVNTarget(np.zeros(D), np.eye(D))
+    np.random.seed(77)
+    q_start = O.start_pts(np.zeros(D), 2 * np.eye(D), N)
+    if sampler_type == "Random":
+        state = np.random.get_state()
+        h = HMC_sampler(D, tgt.V, tgt.dVdq, Nchain=N, Niter=Niter, sampler_type="Random", L_low=5, L_high=20,
+                        dt=0.1, warm_up_num=wu, store_chain=False, stream_tmax=48, iters_per_launch=16,
+                        stream_feed=48)
+        h.gen_sample(q_start, verbose=False)
+        np.random.set_state(state)
+        ref = O.gen_sample_random(O.HMCCore(tgt, 0.1), q_start, N, Niter, wu, 1, 5, 20, O.LiveDraws(D, np.eye(D)))
+        qc = ref["q_chain"]
+        assert np.array_equal(h.E_chain[:, :, 0], ref["E_chain"])
+    else:
+        kw = dict(Nchain=N, Niter=Niter, sampler_type="NUTS", dt=0.2, warm_up_num=wu, rng="philox", seed=5,
+                  fp_mode="fast", iters_per_launch=16)
+        full = HMC_sampler(D, tgt.V, tgt.dVdq, **kw)
+        full.gen_sample(q_start, verbose=False)
+        qc = full.q_chain
+        h = HMC_sampler(D, tgt.V, tgt.dVdq, store_chain=False, stream_tmax=48, stream_feed=48, **kw)
+        h.gen_sample(q_start, verbose=False)
+        assert np.array_equal(h.E_chain, full.E_chain)
+    assert h.q_chain is None
+    h.compute_convergence_stats()
+    R_ref, neff_ref = O.convergence_stats(qc[:, 1:, :], thin_rate=1, warm_up_num=0)
+    np.testing.assert_allclose(h.R_q, R_ref, rtol=1e-10)
+    ok = _lags_needed(qc[:, 1:, :]) <= 64          # stream_tmax 48 -> the 64-lag kernel
+    assert ok.sum() >= 5
+    np.testing.assert_allclose(h.n_eff_q[ok], neff_ref[ok], rtol=1e-10)
+
+
+def test_checkpoint_rejects_other_engine(tmp_path):
+    """A checkpoint restores only into an engine with the same dt, mass matrix and target."""
+    from hmc_amd.engine import RandomEngine
+    from hmc_amd.target import MVNTarget
+    N, D = 64, 12
+    mk = lambda dt, q0: RandomEngine(MVNTarget(q0, np.eye(D)), N, 20, 0, 1, 5, 20, dt, rng="philox",  # noqa: E731
+                                     seed=1, fp_mode="fast")
+    a = mk(0.1, np.zeros(D))
+    a.init(torch.zeros((N, D), dtype=torch.float64).cuda())
+    a.run(1, 5)
+    path = str(tmp_path / "c.npz")
+    a.save(path, 5)
+    assert mk(0.1, np.zeros(D)).restore(path) == 5
+    with pytest.raises(AssertionError, match="dt"):
+        mk(0.2, np.zeros(D)).restore(path)
+    with pytest.raises(AssertionError, match="target_sha256"):
+        mk(0.1, np.full(D, 0.5)).restore(path)

@@ -337,6 +337,7 @@ hipError_t launch_stream_accum(const double* x, int64_t n_chains, int64_t cs, in
     case 8: k_stream_accum<8><<<grid, 256, 0, st>>>(a); break;
     case 16: k_stream_accum<16><<<grid, 256, 0, st>>>(a); break;
     case 32: k_stream_accum<32><<<grid, 256, 0, st>>>(a); break;
+    case 64: k_stream_accum<64><<<grid, 256, 0, st>>>(a); break;
     default: return hipErrorInvalidValue;
   }
   if (hipError_t e = hipGetLastError()) return e;

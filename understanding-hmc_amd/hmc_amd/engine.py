@@ -6,6 +6,7 @@ two calls of the hot path: `init()` (samplers.py:413-420) and `run(it0, it1)`
 (iterations of samplers.py:428-475, fused in one kernel launch).  HMC_sampler
 and bench.py are both thin layers over it.
 """
+import hashlib
 import json
 
 import numpy as np
@@ -49,6 +50,7 @@ class RandomEngine:
         self._minv = None if ident_mass else _dev(minv, dev)
         self._pscale = None if ident_mass else _dev(np.sqrt(np.diag(cov_p)), dev)
         dt = np.asarray(dt, dtype=np.float64)
+        self.dt = dt
         if dt.ndim == 0:
             self._dtv, dts = None, float(dt)
         else:
@@ -139,6 +141,11 @@ class RandomEngine:
         assert feed >= step and feed % step == 0, "feed must be a multiple of step"
         W = T + (feed + step) // self.thin + 2
         st = getattr(self, "_stream", None)
+        if st is not None and st[0] is diag and st[1].shape[1] != W and diag.pos > 0:
+            # the window holds the variogram carry (and possibly written but unfed rows) at
+            # slots r % W_old: a different W would silently drop them
+            raise AssertionError("run_streaming resumed with step/feed giving a %d-row window; the "
+                                 "statistics' window has %d rows (use the same step and feed)" % (W, st[1].shape[1]))
         if st is None or st[0] is not diag or st[1].shape[1] != W:
             st = [diag, torch.zeros((N, W, D), dtype=torch.float64, device=self.device)]
             self._stream = st
@@ -163,9 +170,17 @@ class RandomEngine:
 
     # ---------------------------------------------------------------- checkpoint / resume
     def _meta(self):
+        """Everything that decides the chain's next values: a checkpoint restores only into an
+        engine with the same schedule, step size, mass matrix and target."""
+        t = self.t
+        h = hashlib.sha256()
+        for a in (t.q0, t.prec, np.float64(t.logdet_const)):
+            h.update(np.ascontiguousarray(a, dtype=np.float64).tobytes())
         return dict(kind=type(self).__name__, N=self.N, D=self.D, n_iter=self.n_iter, warm_up=self.warm_up,
-                    thin=self.thin, L_low=self.L_low, L_high=self.L_high, seed=self.seed, rng=self.rng,
-                    fp_mode=self.fp_mode, chain_offset=self.chain_offset, d_max=self.d_max)
+                    thin=self.thin, L_chain=self.L_chain, L_low=self.L_low, L_high=self.L_high, seed=self.seed,
+                    rng=self.rng, fp_mode=self.fp_mode, chain_offset=self.chain_offset, d_max=self.d_max,
+                    dt=np.asarray(self.dt, dtype=np.float64).ravel().tolist(),
+                    cov_p_diag=np.diag(self.cov_p).astype(np.float64).tolist(), target_sha256=h.hexdigest())
 
     def save(self, path, it_next, include_chain=True, diag=None):
         """Checkpoint after iteration it_next - 1 (.npz, no pickles).  Philox draws are keyed by

@@ -23,6 +23,7 @@ import numpy as np
 import torch
 
 from . import _lib as H
+from .diagnostics import StreamingDiagnostics
 from .engine import NutsEngine, RandomEngine
 from .target import MVNTarget, probe_closures  # noqa: F401
 from . import utils as U
@@ -82,7 +83,10 @@ class HMC_sampler(sampler):
       seed     : Philox key (rng="philox")
       fp_mode  : "exact" (reference rounding, no FMA) | "fast" (FMA-contracted integrator)
       device   : torch device (default: current CUDA device)
-      store_chain : keep the full (Nchain, L_chain, D) chain (default True)
+      store_chain : keep the full (Nchain, L_chain, D) chain (default True).  False = streaming
+                    mode: q_chain is None, R_q / n_eff_q come from on-device streamed sums
+      stream_tmax, stream_feed : streaming mode's largest variogram lag and the iterations
+                    between diagnostics updates
       iters_per_launch : iterations fused in one kernel launch (default: all)
       chain_offset : global id of this object's first chain (multi-GPU sharding)
     """
@@ -90,7 +94,8 @@ class HMC_sampler(sampler):
     def __init__(self, D, V, dVdq, Nchain=2, Niter=1000, thin_rate=1, warm_up_num=0,
                  cov_p=None, sampler_type="Fixed", L=None, global_dt=True, dt=None,
                  L_low=None, L_high=None, log2L=None, d_max=10, target=None, rng="replay", seed=0,
-                 fp_mode="exact", device=None, store_chain=True, iters_per_launch=None, chain_offset=0):
+                 fp_mode="exact", device=None, store_chain=True, iters_per_launch=None, chain_offset=0,
+                 stream_tmax=64, stream_feed=60):
         sampler.__init__(self, D=D, target_lnL=None, Nchain=Nchain, Niter=Niter, thin_rate=thin_rate,
                          warm_up_num=warm_up_num)
         self.V = V
@@ -128,6 +133,9 @@ class HMC_sampler(sampler):
         self.seed = int(seed)
         self.fp_mode = fp_mode
         self.store_chain = store_chain
+        self.stream_tmax, self.stream_feed = int(stream_tmax), int(stream_feed)
+        if not store_chain:
+            self.q_chain = None
         self.iters_per_launch = iters_per_launch
         self.chain_offset = int(chain_offset)
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -216,9 +224,7 @@ class HMC_sampler(sampler):
             eng.set_replay(*self._replay_streams_random())
         t0 = time.time()
         eng.init(q_start.reshape(self.Nchain, self.D))
-        step = self.iters_per_launch or self.Niter
-        for it0 in range(1, self.Niter + 1, step):
-            eng.run(it0, min(it0 + step, self.Niter + 1))
+        self._run(eng)
         torch.cuda.synchronize(self.device)
         elapsed = time.time() - t0
         self._finish(eng, elapsed, verbose)
@@ -230,6 +236,39 @@ class HMC_sampler(sampler):
         print("After warm up: %.3f" % self.accept_R)
         print("Completed.")
         return
+
+    def _run(self, eng):
+        """All Niter iterations.  With store_chain the whole q_chain stays on the device and one
+        launch covers `iters_per_launch` iterations (default: the whole run).  Without it
+        (streaming mode) the rows go to a circular device window that feeds
+        StreamingDiagnostics after every `stream_feed` iterations, so memory is
+        O(Nchain * (stream_tmax + window) * D) and compute_convergence_stats() reads the
+        streamed sums instead of a q_chain."""
+        self._stream_diag = None
+        if self.store_chain:
+            step = self.iters_per_launch or self.Niter
+            for it0 in range(1, self.Niter + 1, step):
+                eng.run(it0, min(it0 + step, self.Niter + 1))
+            return
+        n_samples = self.L_chain - 1
+        if n_samples < 4:
+            raise AssertionError("streaming statistics need L_chain - 1 >= 4 samples per chain")
+        tmax = next(t for t in (8, 16, 32, 64) if t >= min(int(self.stream_tmax), 64))   # kernel lag rings
+        diag = StreamingDiagnostics(self.Nchain, self.D, n_samples, tmax=tmax, device=self.device)
+        step = self.iters_per_launch or 20
+        feed = max(step, (int(self.stream_feed) // step) * step)
+        eng.run_streaming(diag, 1, self.Niter + 1, step, feed=feed)
+        self._stream_diag = diag
+
+    def compute_convergence_stats(self):
+        """samplers.py:53-64.  In streaming mode (store_chain=False) the split-chain sums were
+        accumulated on the device during the run: R-hat is exact, the ESS sum stops at lag
+        stream_tmax if the reference's criterion has not fired by then."""
+        diag = getattr(self, "_stream_diag", None)
+        if diag is not None:
+            self.R_q, self.n_eff_q = diag.finish()
+            return
+        sampler.compute_convergence_stats(self)
 
     def _finish(self, eng, elapsed, verbose):
         """Copy results to the reference's NumPy attributes and derive the counters."""
@@ -248,6 +287,8 @@ class HMC_sampler(sampler):
         self.q_device = eng.q
         if eng.q_chain is not None:
             self.q_chain = eng.q_chain.cpu().numpy()
+        else:
+            self.q_chain = None                     # streaming mode: statistics only
         self.E_chain = eng.E_chain.cpu().numpy()[:, :, None]
         self.dE_chain = eng.dE_chain.cpu().numpy()[:, :, None]
         if eng.n_save:
@@ -288,9 +329,7 @@ class HMC_sampler(sampler):
             eng.set_replay(*tape)
         t0 = time.time()
         eng.init(q_start.reshape(self.Nchain, self.D))
-        step = self.iters_per_launch or self.Niter
-        for it0 in range(1, self.Niter + 1, step):
-            eng.run(it0, min(it0 + step, self.Niter + 1))
+        self._run(eng)
         torch.cuda.synchronize(self.device)
         elapsed = time.time() - t0
         c = eng.read_counters()
@@ -309,8 +348,7 @@ class HMC_sampler(sampler):
         self.engine = eng
         self.q_chain_device = eng.q_chain
         self.q_device = eng.q
-        if eng.q_chain is not None:
-            self.q_chain = eng.q_chain.cpu().numpy()
+        self.q_chain = eng.q_chain.cpu().numpy() if eng.q_chain is not None else None
         self.E_chain = eng.E_chain.cpu().numpy()[:, :, None]
         self.dE_chain = eng.dE_chain.cpu().numpy()[:, :, None]
         print("Compute acceptance rate: By default equal to 1.")                 # :800-805
