@@ -76,6 +76,13 @@ typedef struct hmc_kinetic {
   const double* p_scale;   /* [D] sqrt(diag(cov_p)) for in-kernel draws, NULL => 1        */
   const double* dt_vec;    /* [D] per-dimension step (global_dt=False), NULL => dt        */
   double dt;               /* scalar step                                                 */
+  /* Dense (non-diagonal) mass matrix, samplers.py:352-356 with a full cov_p (Q3 semantics:
+   * K = p.inv(cov_p).p/2, kick by inv(cov_p).dVdq, drift by p).  All NULL => diagonal/identity
+   * via minv/p_scale above (which must then be NULL).  Random sampler, dense targets only.  */
+  const double* minv_full; /* [D*D] inv(cov_p), row-major (symmetric)                     */
+  const double* p_chol_t;  /* [D*D] transpose of the lower Cholesky factor C of cov_p:
+                              Philox momentum p = C z, z ~ N(0, I)                        */
+  const double* kick;      /* [D*D] inv(cov_p) . prec, row-major: the kick matrix          */
 } hmc_kinetic;
 
 /* Run schedule of gen_sample_random / gen_sample_NUTS (samplers.py:387, :495). */

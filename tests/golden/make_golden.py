@@ -28,6 +28,8 @@ import numpy as np
 import scipy
 
 REF = "/root/reference"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from make_golden_shapes import dense_cov_p  # noqa: E402
 OUT = os.path.dirname(os.path.abspath(__file__))
 
 np.float = float  # removed alias used at samplers.py:33, :359-360 (Python-2/NumPy<1.24 era)
@@ -294,6 +296,8 @@ if __name__ == "__main__":
                L_low=5, L_high=20, dt=0.1, seed=6, start_scale=100.0, case2_override=True, n_save=20)
     run_random("f11_case5_unstable", D=10, rho=0.999, Nchain=3, Niter=120, wu=40, thin=1,
                L_low=5, L_high=20, dt=0.1, seed=8)
+    run_random("f12_dense_covp", D=12, rho=0.6, Nchain=3, Niter=90, wu=30, thin=1,
+               L_low=5, L_high=20, dt=0.1, seed=12, cov_p=dense_cov_p(12))
     run_nuts("f6_nuts_dense100", D=100, rho=0.95, Nchain=2, Niter=12, wu=4, thin=1, dt=0.1,
              d_max=12, seed=9)
     run_leapfrog_vectors()

@@ -35,7 +35,7 @@ def test_struct_layouts():
     from hmc_amd import _lib as H
     # sizes follow from the C declarations (x86-64 SysV alignment)
     assert ctypes.sizeof(H.Target) == 32
-    assert ctypes.sizeof(H.Kinetic) == 32
+    assert ctypes.sizeof(H.Kinetic) == 56
     assert ctypes.sizeof(H.Schedule) == 8 + 8 + 12 * 4 + 8
     assert ctypes.sizeof(H.Replay) == 48
     assert ctypes.sizeof(H.State) == 9 * 8 + 8 + 2 * 8 + 8

@@ -282,7 +282,8 @@ def test_wave_kernel_replay_exact_vs_oracle(D, thin, wu, gen):
     assert h.N_total_steps == ref["N_total_steps"]
 
 
-DENSE_FIXTURES = ["f3_case3c_small.npz", "f3b_case3a.npz", "f11_case5_unstable.npz"]
+DENSE_FIXTURES = ["f3_case3c_small.npz", "f3b_case3a.npz", "f11_case5_unstable.npz",
+                  "f12_dense_covp.npz"]   # f12: full (non-diagonal) cov_p, Q3 (samplers.py:352-356, :825-839)
 
 
 @pytest.mark.parametrize("fx", DENSE_FIXTURES)
@@ -363,3 +364,42 @@ def test_dense_L_ordered_tiles_identical(rng, fp_mode):
                     eng.q.cpu().numpy(), eng.read_counters()])
     for a, b in zip(*out):
         assert np.array_equal(a, b)
+
+
+def test_dense_mass_matrix_rows_and_stationarity():
+    """Full cov_p (Q3: K = p.inv(cov_p).p/2, p ~ N(0, cov_p), kick by inv(cov_p).dVdq, drift by
+    p).  Row API vs the oracle's HMCCore (samplers.py:811-839) to round-off; Philox chains
+    started in N(0, Sigma) stay there (the reference's proposal is a reversible volume-preserving
+    map with an exact MH correction, so the target is invariant) and are deterministic."""
+    from hmc_amd.samplers import HMC_sampler
+    from hmc_amd.target import MVNTarget
+    import make_golden_shapes as S
+    D, rho = 12, 0.6
+    cov, cov_p = O.mvn_cov(D, rho), S.dense_cov_p(D)
+    tgt = O.MVNTarget(np.zeros(D), cov)
+    core = O.HMCCore(tgt, 0.1, cov_p)
+    rs = np.random.RandomState(5)
+    P, Q = rs.standard_normal((4, D)), rs.standard_normal((4, D))
+    h = HMC_sampler(D, tgt.V, tgt.dVdq, Nchain=2, Niter=1, sampler_type="Random", L_low=1, L_high=2, dt=0.1,
+                    cov_p=cov_p, target=MVNTarget(np.zeros(D), cov))
+    pn, qn = h.leap_frog(P, Q)
+    for i in range(4):
+        pr, qr = core.leap_frog(P[i], Q[i])
+        np.testing.assert_allclose(pn[i], pr, rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(qn[i], qr, rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(h.E(Q[i], P[i]), core.E(Q[i], P[i]), rtol=1e-12)
+    N = 8192
+    q0 = rs.standard_normal((N, D)) @ np.linalg.cholesky(cov).T
+
+    def run():
+        s = HMC_sampler(D, None, None, Nchain=N, Niter=10, sampler_type="Random", L_low=5, L_high=20, dt=0.1,
+                        warm_up_num=2, cov_p=cov_p, target=MVNTarget(np.zeros(D), cov), rng="philox", seed=3,
+                        fp_mode="fast")
+        s.gen_sample(q0, verbose=False)
+        return s
+    a = run()
+    last = a.q_chain[:, -1, :]
+    assert np.abs(last.var(axis=0) - 1).max() < 6 * np.sqrt(2 / N)
+    assert abs(np.corrcoef(last[:, 0], last[:, 1])[0, 1] - rho) < 6 * (1 - rho ** 2) / np.sqrt(N)
+    assert 0.05 < a.accept_R < 1.0
+    assert np.array_equal(a.q_chain, run().q_chain)

@@ -14,7 +14,7 @@ from oracle import hmc_oracle as O
 
 RANDOM_FIXTURES = ["f1_case1a.npz", "f2_case1c_small.npz", "f3_case3c_small.npz", "f3b_case3a.npz",
                    "f8_diag_thin_vecdt.npz", "f9_wu0_thin2.npz", "f10_case2a.npz",
-                   "f11_case5_unstable.npz"]
+                   "f11_case5_unstable.npz", "f12_dense_covp.npz"]
 
 
 def _core(g):

@@ -25,6 +25,22 @@ __device__ __forceinline__ double grad_d(const RowArgs& a, const double* q, int 
   return a.prec ? a.prec[d] * x : x;
 }
 
+// (inv(cov_p) dVdq(q))_d: the diagonal mass scales g_d; a dense one (minvf) takes the row
+// product with every g_j, recomputed on the fly (O(D^3) per row: these are parity-size calls).
+template <bool EXACT>
+__device__ __forceinline__ double kick_d(const RowArgs& a, const double* q, int d) {
+  if (a.minvf) {
+    const double* Mr = a.minvf + (int64_t)d * a.D;
+    double acc = 0.0;
+    for (int j = 0; j < a.D; ++j) {
+      const double g = grad_d<EXACT>(a, q, j);
+      acc = EXACT ? acc + Mr[j] * g : __builtin_fma(Mr[j], g, acc);
+    }
+    return acc;
+  }
+  return a.minv ? a.minv[d] * grad_d<EXACT>(a, q, d) : grad_d<EXACT>(a, q, d);
+}
+
 template <bool EXACT>
 __global__ __launch_bounds__(256) void k_leapfrog_rows(RowArgs a) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -35,8 +51,7 @@ __global__ __launch_bounds__(256) void k_leapfrog_rows(RowArgs a) {
   double* qo = a.qo + r * a.D;
   for (int d = 0; d < a.D; ++d) {       // p_half = p_old - dt*(Minv dVdq(q_old))/2
     const double dt = a.dtv ? a.dtv[d] : a.dt;
-    const double x = a.minv ? a.minv[d] * grad_d<EXACT>(a, q, d) : grad_d<EXACT>(a, q, d);
-    po[d] = p[d] - (dt * x) * 0.5;
+    po[d] = p[d] - (dt * kick_d<EXACT>(a, q, d)) * 0.5;
   }
   for (int d = 0; d < a.D; ++d) {       // q_new = q_old + dt*p_half
     const double dt = a.dtv ? a.dtv[d] : a.dt;
@@ -44,8 +59,7 @@ __global__ __launch_bounds__(256) void k_leapfrog_rows(RowArgs a) {
   }
   for (int d = 0; d < a.D; ++d) {       // p_new = p_half - dt*(Minv dVdq(q_new))/2
     const double dt = a.dtv ? a.dtv[d] : a.dt;
-    const double x = a.minv ? a.minv[d] * grad_d<EXACT>(a, qo, d) : grad_d<EXACT>(a, qo, d);
-    po[d] = po[d] - (dt * x) * 0.5;
+    po[d] = po[d] - (dt * kick_d<EXACT>(a, qo, d)) * 0.5;
   }
 }
 
@@ -58,7 +72,14 @@ __global__ __launch_bounds__(256) void k_energy_rows(RowArgs a) {
   for (int d = 0; d < a.D; ++d) {
     const double x = q[d] - (a.q0 ? a.q0[d] : 0.0);
     maha += x * grad_d<true>(a, q, d);
-    kin += p[d] * (a.minv ? a.minv[d] * p[d] : p[d]);
+    if (a.minvf) {
+      const double* Mr = a.minvf + (int64_t)d * a.D;
+      double mp = 0.0;
+      for (int j = 0; j < a.D; ++j) mp += Mr[j] * p[j];
+      kin += p[d] * mp;
+    } else {
+      kin += p[d] * (a.minv ? a.minv[d] * p[d] : p[d]);
+    }
   }
   a.E[r] = 0.5 * (a.logc + maha) + kin / 2.0;
 }

@@ -69,6 +69,17 @@ hmc_status check_window(const hmc_target* t, const hmc_schedule* s, const hmc_st
   return HMC_OK;
 }
 
+// Dense mass matrix (full cov_p, samplers.py:352-356): only the dense-target Random kernels take it.
+hmc_status check_mass(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s) {
+  if (!k->minv_full && !k->p_chol_t && !k->kick) return HMC_OK;
+  if (!k->minv_full || !k->kick) return fail(HMC_EINVAL, "dense mass matrix needs minv_full and kick");
+  if (k->minv || k->p_scale) return fail(HMC_EINVAL, "dense mass matrix: minv/p_scale must be NULL");
+  if (t->kind != HMC_TARGET_DENSE) return fail(HMC_ENOTSUP, "dense mass matrix needs a dense target (pass prec dense)");
+  if (s && s->rng_mode == HMC_RNG_PHILOX && !k->p_chol_t)
+    return fail(HMC_EINVAL, "dense mass matrix with Philox draws needs p_chol_t");
+  return HMC_OK;
+}
+
 hmc::RandArgs rand_args(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, const hmc_replay* r,
                         hmc_state* st, const hmc::Layout& lay) {
   hmc::RandArgs a{};
@@ -98,6 +109,9 @@ hmc::RandArgs rand_args(const hmc_target* t, const hmc_kinetic* k, const hmc_sch
   a.minv = k->minv;
   a.pscale = k->p_scale;
   a.dtv = k->dt_vec;
+  a.minvf = k->minv_full;
+  a.cholt = k->p_chol_t;
+  a.kick = k->kick;
   if (r) {
     a.rp0 = r->p0;
     a.rp = r->p;
@@ -163,6 +177,7 @@ hmc_status hmc_chain_init(const hmc_target* t, const hmc_kinetic* k, const hmc_s
                           const double* q_start, hmc_state* st, void* stream) {
   if (hmc_status e = check_schedule(t, k, s, false)) return e;
   if (!st) return fail(HMC_EINVAL, "null state");
+  if (hmc_status e = check_mass(t, k, s)) return e;
   if (s->n_chains == 0) return HMC_OK;   // empty batch: zero-size buffers may be NULL
   if (!st->q || !st->E_prev || !q_start) return fail(HMC_EINVAL, "null state/q_start");
   const bool replay = s->rng_mode == HMC_RNG_REPLAY;
@@ -189,6 +204,7 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
   if (hmc_status e = check_schedule(t, k, s, true)) return e;
   if (!st) return fail(HMC_EINVAL, "null state");
   if (hmc_status e = check_window(t, s, st)) return e;
+  if (hmc_status e = check_mass(t, k, s)) return e;
   if (s->iter_begin < 1 || s->iter_end < s->iter_begin || s->iter_end > s->n_iter + 1)
     return fail(HMC_EINVAL, "iteration range must satisfy 1 <= begin <= end <= Niter+1");
   if (s->n_chains == 0) return HMC_OK;   // empty batch: zero-size buffers may be NULL
@@ -259,6 +275,8 @@ hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_s
   if (s->n_chains == 0) return HMC_OK;   // empty batch: zero-size buffers may be NULL
   if (!st->q || !st->E_prev) return fail(HMC_EINVAL, "null state");
   if (s->d_max < 1 || s->d_max > 15) return fail(HMC_EINVAL, "d_max must be in [1, 15]");
+  if (k->minv_full || k->p_chol_t || k->kick)
+    return fail(HMC_ENOTSUP, "NUTS: dense (non-diagonal) mass matrix not supported");
   if (t->kind != HMC_TARGET_DENSE) return fail(HMC_ENOTSUP, "NUTS runs the dense kernel: pass prec as dense");
   if (!hmc::dense_tiles(t->D)) return fail(HMC_ENOTSUP, "dense target: D=%d > 128 not supported", t->D);
   const bool replay = s->rng_mode == HMC_RNG_REPLAY;
@@ -291,7 +309,9 @@ hmc_status hmc_leapfrog(const hmc_target* t, const hmc_kinetic* k, int64_t n, co
   a.dense = t->kind == HMC_TARGET_DENSE;
   a.q0 = t->q0;
   a.prec = t->prec;
+  if (hmc_status e = check_mass(t, k, nullptr)) return e;
   a.minv = k->minv;
+  a.minvf = k->minv_full;
   a.dtv = k->dt_vec;
   a.dt = k->dt;
   a.logc = t->logdet_const;
@@ -312,7 +332,9 @@ hmc_status hmc_energy(const hmc_target* t, const hmc_kinetic* k, int64_t n, cons
   a.dense = t->kind == HMC_TARGET_DENSE;
   a.q0 = t->q0;
   a.prec = t->prec;
+  if (hmc_status e = check_mass(t, k, nullptr)) return e;
   a.minv = k->minv;
+  a.minvf = k->minv_full;
   a.logc = t->logdet_const;
   a.p = p;
   a.q = q;

@@ -27,7 +27,9 @@ namespace {
 
 // WAVES waves per block, one block per CU (the LDS copy of P); WAVES = 4: one wave per SIMD
 // with the whole 512-register file.
-template <int MT, bool EXACT, bool GEN, bool REPLAY, int WAVES>
+// MASS: dense (non-diagonal) mass matrix (implies GEN): its own instantiation, so the extra
+// products' registers never touch the diagonal-mass kernels.
+template <int MT, bool EXACT, bool GEN, bool REPLAY, int WAVES, bool MASS = false>
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVES / 4, WAVES / 4)))
 void k_dense_iters(DenseArgs a) {
   constexpr int M = 4 * MT;
@@ -96,17 +98,42 @@ void k_dense_iters(DenseArgs a) {
         p[m + 1] = dim_ok(m + 1) ? z1 : 0.0;
         if ((m & 6) == 6) __builtin_amdgcn_sched_barrier(0);   // bound the RNG chains in flight (registers)
       }
+      if constexpr (MASS) {   // dense mass matrix: p = C z ~ N(0, cov_p) (samplers.py:829)
+        d4 cz[MT];
+        matvec_global<MT>(a.cholt, a.D, lane, p, cz);
+#pragma unroll
+        for (int m = 0; m < M; ++m) p[m] = dim_ok(m) ? gval<MT>(cz, m) : 0.0;
+      }
     }
     // ---- gradient at q and E0 = V(q) + K(p)  (:434)
     gradient<MT, GEN>(a, sP, lane, h, q, acc);
     double maha = 0.0, kin = 0.0;
+    // (x . P x, p . Minv p) of this lane's dims.  Diagonal/identity mass: P x is the gradient
+    // tile.  Dense mass: the tile holds Minv P x (the kick), so P x and Minv p are two more
+    // products (samplers.py:811-823 with a full inv_cov_p).
+    auto energy_terms = [&](double& mh, double& kn) {
+      if constexpr (MASS) {
+        double xv[M];
 #pragma unroll
-    for (int m = 0; m < M; ++m) {       // padded dims contribute exact zeros (g = p = 0)
-      const int d = h + 4 * m;
-      const double x = (GEN && a.q0) ? q[m] - a.q0[min(d, a.D - 1)] : q[m];
-      maha += x * gval<MT>(acc, m);
-      kin += p[m] * (dim_minv<MT, GEN>(a, d) * p[m]);
-    }
+        for (int m = 0; m < M; ++m) xv[m] = a.q0 ? q[m] - a.q0[min(h + 4 * m, a.D - 1)] : q[m];
+        d4 t[MT];
+        matvec_global<MT>(a.prec, a.D, lane, xv, t);
+#pragma unroll
+        for (int m = 0; m < M; ++m) mh += xv[m] * gval<MT>(t, m);
+        matvec_global<MT>(a.minvf, a.D, lane, p, t);
+#pragma unroll
+        for (int m = 0; m < M; ++m) kn += p[m] * gval<MT>(t, m);
+        return;
+      }
+#pragma unroll
+      for (int m = 0; m < M; ++m) {       // padded dims contribute exact zeros (g = p = 0)
+        const int d = h + 4 * m;
+        const double x = (GEN && a.q0) ? q[m] - a.q0[min(d, a.D - 1)] : q[m];
+        mh += x * gval<MT>(acc, m);
+        kn += p[m] * (dim_minv<MT, GEN>(a, d) * p[m]);
+      }
+    };
+    energy_terms(maha, kin);
     const double E0 = 0.5 * (a.logc + chain_sum4(maha + kin));
     const bool post = it >= a.wu;
     const bool write_row = post && ((it == a.niter) || ((it - a.wu + 1) % a.thin == 0));
@@ -186,13 +213,7 @@ void k_dense_iters(DenseArgs a) {
     // ---- E1 with the gradient of the final q, Metropolis test (:455-472)
     maha = 0.0;
     kin = 0.0;
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const int d = h + 4 * m;
-      const double x = (GEN && a.q0) ? q[m] - a.q0[min(d, a.D - 1)] : q[m];
-      maha += x * gval<MT>(acc, m);
-      kin += p[m] * (dim_minv<MT, GEN>(a, d) * p[m]);
-    }
+    energy_terms(maha, kin);
     const double E1 = 0.5 * (a.logc + chain_sum4(maha + kin));
     const double dE = E1 - E0;
     const bool accept = (dE < 0.0) || (lnu < -dE);
@@ -242,6 +263,41 @@ void k_dense_iters(DenseArgs a) {
   }
 }
 
+// p0 . inv(cov_p) . p0 of the initial momentum with a dense mass matrix (samplers.py:415-416):
+// p0 = C z with z in the dims' Philox mapping (or the replayed p0).  One thread per chain, O(D^2).
+template <bool REPLAY>
+__device__ double dense_mass_kinetic0(const DenseArgs& a, int64_t c, uint64_t gc, int MT) {
+  const int D = a.D;
+  double p0[128];   // D <= 128 (dense_tiles)
+  for (int d = 0; d < D; ++d) p0[d] = 0.0;
+  if constexpr (REPLAY) {
+    for (int d = 0; d < D; ++d) p0[d] = a.rp0[c * D + d];
+  } else {
+    double z[128];
+    const int M = 4 * MT;
+    for (int h = 0; h < 4; ++h)
+      for (int m = 0; m < M; m += 2) {
+        const int d0 = h + 4 * m, d1 = d0 + 4;
+        double z0, z1;
+        normal_pair(draw_block((uint32_t)(h + 4 * m), 0u, gc, a.k0, a.k1), z0, z1);
+        if (d0 < D) z[d0] = z0;
+        if (d1 < D) z[d1] = z1;
+      }
+    for (int r = 0; r < D; ++r) {
+      double acc = 0.0;
+      for (int k = 0; k <= r; ++k) acc = __builtin_fma(a.cholt[(int64_t)k * D + r], z[k], acc);   // C[r][k]
+      p0[r] = acc;
+    }
+  }
+  double kin = 0.0;
+  for (int r = 0; r < D; ++r) {
+    double mp = 0.0;
+    for (int k = 0; k < D; ++k) mp = __builtin_fma(a.minvf[(int64_t)r * D + k], p0[k], mp);
+    kin += p0[r] * mp;
+  }
+  return kin;
+}
+
 // Chain initialisation for dense targets (samplers.py:413-420), one thread per chain.
 template <bool REPLAY>
 __global__ __launch_bounds__(256) void k_dense_init(DenseArgs a, int MT) {
@@ -271,10 +327,12 @@ __global__ __launch_bounds__(256) void k_dense_init(DenseArgs a, int MT) {
           z1 = d1 < a.D ? z1 * a.pscale[d1] : 0.0;
         }
       }
+      if (a.minvf) continue;   // dense mass: K from the whole vector below
       if (d0 < a.D) kin += z0 * ((a.minv ? a.minv[d0] : 1.0) * z0);
       if (d1 < a.D && m + 1 < M) kin += z1 * ((a.minv ? a.minv[d1] : 1.0) * z1);
     }
   }
+  if (a.minvf) kin = dense_mass_kinetic0<REPLAY>(a, c, gc, MT);
   const double E0 = 0.5 * (a.logc + (maha + kin));
   for (int d = 0; d < a.D; ++d) {
     a.q[c * a.D + d] = qs[d];
@@ -347,7 +405,10 @@ void launch_dense_w(const DenseArgs& a, bool gen, bool replay, hipStream_t s) {
   const int64_t blocks = (a.ntiles + WAVES - 1) / WAVES;
   const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)device_cus())));
   const size_t lds = (size_t)MT * 4 * MT * kWave * sizeof(double);
-  if (gen) {
+  if (a.minvf) {
+    if (replay) k_dense_iters<MT, EXACT, true, true, WAVES, true><<<grid, 64 * WAVES, lds, s>>>(a);
+    else k_dense_iters<MT, EXACT, true, false, WAVES, true><<<grid, 64 * WAVES, lds, s>>>(a);
+  } else if (gen) {
     if (replay) k_dense_iters<MT, EXACT, true, true, WAVES><<<grid, 64 * WAVES, lds, s>>>(a);
     else k_dense_iters<MT, EXACT, true, false, WAVES><<<grid, 64 * WAVES, lds, s>>>(a);
   } else {
@@ -416,7 +477,7 @@ hipError_t launch_dense_order(const DenseArgs& a, int it, bool replay, int32_t* 
 }
 
 hipError_t launch_dense_iters(const DenseArgs& a, bool exact, bool replay, hipStream_t s) {
-  const bool gen = a.q0 || a.minv || a.pscale || a.dtv;
+  const bool gen = a.q0 || a.minv || a.pscale || a.dtv || a.minvf;
   switch (dense_tiles(a.D)) {
     case 1: return launch_dense_mt<1>(a, exact, gen, replay, s);
     case 2: return launch_dense_mt<2>(a, exact, gen, replay, s);

@@ -73,6 +73,48 @@ __device__ __forceinline__ void gradient(const DenseArgs& a, const double* __res
   }
 }
 
+// y = M x for a symmetric (or pre-transposed) row-major D x D matrix in global memory (L2-resident),
+// in the gradient's lane layout: the A-operand element (row 16nt + c, col 4ks + h) is read as
+// src[(4ks + h) * D + 16nt + c], 16 consecutive doubles per (ks, h): 4 x 128 B per fragment.
+// For symmetric M this is M[row][col]; pass the transpose of a non-symmetric matrix.  Used by the
+// dense-mass-matrix path only (3-5 products per iteration against 13 LDS gradients), so the
+// fragments come from L2 with a PF-deep prefetch instead of taking the LDS the kick matrix holds.
+template <int MT>
+__device__ __forceinline__ void matvec_global(const double* __restrict__ src, int D, int lane,
+                                              const double (&x)[4 * MT], d4 (&acc)[MT]) {
+  constexpr int KS = 4 * MT;
+  constexpr int PF = 4;
+  const int c = lane & 15, h = lane >> 4;
+  const int ks_end = __builtin_amdgcn_readfirstlane((D + 3) >> 2);
+  auto load = [&](int nt, int ks) -> double {
+    const int row = 16 * nt + c, col = 4 * ks + h;
+    const double v = src[(int64_t)min(col, D - 1) * D + min(row, D - 1)];
+    return (row < D && col < D) ? v : 0.0;
+  };
+  double buf[PF][MT];
+#pragma unroll
+  for (int nt = 0; nt < MT; ++nt) acc[nt] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int j = 0; j < PF; ++j) {
+#pragma unroll
+    for (int nt = 0; nt < MT; ++nt) buf[j][nt] = j < KS ? load(nt, j) : 0.0;
+  }
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (ks >= KS - 3 && ks >= ks_end) break;   // only the last 3 k-steps can be all padding
+    double cur[MT];
+#pragma unroll
+    for (int nt = 0; nt < MT; ++nt) cur[nt] = buf[ks % PF][nt];
+    if (ks + PF < KS) {
+#pragma unroll
+      for (int nt = 0; nt < MT; ++nt) buf[ks % PF][nt] = load(nt, ks + PF);
+    }
+#pragma unroll
+    for (int nt = 0; nt < MT; ++nt) acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[nt], x[ks], acc[nt], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 template <int MT>
 __device__ __forceinline__ double gval(const d4 (&acc)[MT], int m) {
   return acc[m >> 2][m & 3];
@@ -93,14 +135,16 @@ __device__ __forceinline__ double dim_dt(const DenseArgs& a, int d) {
 
 // P fragments -> LDS (zero padded): fragment (nt, ks) lane l holds P[16nt + (l&15)][4ks + (l>>4)],
 // stored lane-linear so every MFMA A-operand read is one conflict-free ds_read_b64.
+// With a dense mass matrix the staged matrix is the kick matrix inv(cov_p).prec (a.kick).
 template <int MT>
 __device__ __forceinline__ void stage_precision(const DenseArgs& a, double* sP) {
   constexpr int KS = 4 * MT;
+  const double* src = a.kick ? a.kick : a.prec;
   for (int f = threadIdx.x; f < MT * KS * kWave; f += blockDim.x) {
     const int l = f & (kWave - 1), t = f / kWave;
     const int nt = t / KS, ks = t - nt * KS;
     const int n = 16 * nt + (l & 15), k = 4 * ks + (l >> 4);
-    sP[f] = (n < a.D && k < a.D) ? a.prec[(int64_t)n * a.D + k] : 0.0;
+    sP[f] = (n < a.D && k < a.D) ? src[(int64_t)n * a.D + k] : 0.0;
   }
   __syncthreads();
 }

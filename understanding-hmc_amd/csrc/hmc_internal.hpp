@@ -28,6 +28,9 @@ struct RandArgs {
   const double* minv;    // [D] or null
   const double* pscale;  // [D] or null
   const double* dtv;     // [D] or null
+  const double* minvf;   // dense mass: [D*D] inv(cov_p) (symmetric) or null
+  const double* cholt;   // dense mass: [D*D] transpose of chol(cov_p) (Philox draws)
+  const double* kick;    // dense mass: [D*D] inv(cov_p) . prec (staged in LDS instead of prec)
   const double* rp0;     // replay streams
   const double* rp;
   const double* rlnu;
@@ -85,6 +88,7 @@ struct RowArgs {
   const double* prec;
   const double* minv;
   const double* dtv;
+  const double* minvf;   // dense mass matrix inv(cov_p) [D*D] or null
   double dt, logc;
   const double* p;
   const double* q;

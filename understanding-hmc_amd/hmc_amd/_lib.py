@@ -27,7 +27,8 @@ class Target(ctypes.Structure):
 
 
 class Kinetic(ctypes.Structure):
-    _fields_ = [("minv", c_dp), ("p_scale", c_dp), ("dt_vec", c_dp), ("dt", ctypes.c_double)]
+    _fields_ = [("minv", c_dp), ("p_scale", c_dp), ("dt_vec", c_dp), ("dt", ctypes.c_double),
+                ("minv_full", c_dp), ("p_chol_t", c_dp), ("kick", c_dp)]
 
 
 class Schedule(ctypes.Structure):

@@ -34,21 +34,30 @@ class RandomEngine:
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         dev = self.device
         # ---- target / kinetic descriptors (kept alive on the object)
-        diag = target.diagonal and not dense
+        cov_p = np.diag(np.ones(D)) if cov_p is None else np.asarray(cov_p, dtype=np.float64)
+        self.cov_p = cov_p
+        full_mass = bool(np.any(cov_p - np.diag(np.diag(cov_p))))   # Q3 with a full cov_p
+        diag = target.diagonal and not dense and not full_mass
         kind = H.HMC_TARGET_DIAG if diag else H.HMC_TARGET_DENSE
         self._q0 = None if target.zero_mean else _dev(target.q0, dev)
         if diag:
             self._prec = None if target.identity else _dev(np.diag(target.prec), dev)
         else:
             self._prec = _dev(target.prec, dev)
-        cov_p = np.diag(np.ones(D)) if cov_p is None else np.asarray(cov_p, dtype=np.float64)
-        if np.any(cov_p - np.diag(np.diag(cov_p))):
-            raise NotImplementedError("non-diagonal cov_p: the GPU kernels support a diagonal mass matrix")
-        self.cov_p = cov_p
-        minv = np.diag(np.linalg.inv(cov_p)).astype(np.float64)      # samplers.py:356
-        ident_mass = bool(np.all(np.diag(cov_p) == 1.0) and np.all(minv == 1.0))
-        self._minv = None if ident_mass else _dev(minv, dev)
-        self._pscale = None if ident_mass else _dev(np.sqrt(np.diag(cov_p)), dev)
+        self._minv_full = self._chol_t = self._kick = None
+        if full_mass:
+            # samplers.py:356 (inv_cov_p), :829 (p ~ N(0, cov_p) = C z) and :835-837 (kick by
+            # inv_cov_p . dVdq): host-side constants of the run, like the reference's inv_cov_p
+            minv_full = np.linalg.inv(cov_p)
+            self._minv_full = _dev(minv_full, dev)
+            self._chol_t = _dev(np.linalg.cholesky(cov_p).T, dev)
+            self._kick = _dev(minv_full @ np.asarray(target.prec, dtype=np.float64), dev)
+            self._minv = self._pscale = None
+        else:
+            minv = np.diag(np.linalg.inv(cov_p)).astype(np.float64)      # samplers.py:356
+            ident_mass = bool(np.all(np.diag(cov_p) == 1.0) and np.all(minv == 1.0))
+            self._minv = None if ident_mass else _dev(minv, dev)
+            self._pscale = None if ident_mass else _dev(np.sqrt(np.diag(cov_p)), dev)
         dt = np.asarray(dt, dtype=np.float64)
         self.dt = dt
         if dt.ndim == 0:
@@ -57,7 +66,8 @@ class RandomEngine:
             assert dt.size == D
             self._dtv, dts = _dev(dt.reshape(-1), dev), 0.0
         self.T = H.Target(D, kind, H.ptr(self._q0), H.ptr(self._prec), target.logdet_const)
-        self.K = H.Kinetic(H.ptr(self._minv), H.ptr(self._pscale), H.ptr(self._dtv), dts)
+        self.K = H.Kinetic(H.ptr(self._minv), H.ptr(self._pscale), H.ptr(self._dtv), dts, H.ptr(self._minv_full),
+                           H.ptr(self._chol_t), H.ptr(self._kick))
         # ---- state and outputs
         N, Lc = self.N, self.L_chain
         self.q = torch.zeros((N, D), dtype=torch.float64, device=dev)
@@ -180,7 +190,8 @@ class RandomEngine:
                     thin=self.thin, L_chain=self.L_chain, L_low=self.L_low, L_high=self.L_high, seed=self.seed,
                     rng=self.rng, fp_mode=self.fp_mode, chain_offset=self.chain_offset, d_max=self.d_max,
                     dt=np.asarray(self.dt, dtype=np.float64).ravel().tolist(),
-                    cov_p_diag=np.diag(self.cov_p).astype(np.float64).tolist(), target_sha256=h.hexdigest())
+                    cov_p_sha256=hashlib.sha256(np.ascontiguousarray(self.cov_p, np.float64).tobytes()).hexdigest(),
+                    target_sha256=h.hexdigest())
 
     def save(self, path, it_next, include_chain=True, diag=None):
         """Checkpoint after iteration it_next - 1 (.npz, no pickles).  Philox draws are keyed by
@@ -242,6 +253,8 @@ class NutsEngine(RandomEngine):
                          fp_mode=fp_mode, chain_offset=chain_offset, store_chain=store_chain,
                          store_energy=store_energy, n_save=0, device=device, dense=True)
         assert on_dmax in ("raise", "break")
+        if self._minv_full is not None:
+            raise NotImplementedError("NUTS kernel: non-diagonal cov_p is not supported (Random sampler only)")
         self.d_max = int(d_max)
         self.on_dmax = 0 if on_dmax == "raise" else 1
         nbytes = H.lib().hmc_nuts_workspace_size(self.D, self.N, self.d_max)

@@ -153,28 +153,34 @@ class HMC_sampler(sampler):
         t = self.target()
         dev = self.device
         keep = []
-        kind = H.HMC_TARGET_DIAG if t.diagonal else H.HMC_TARGET_DENSE
+        cov_p = np.asarray(self.cov_p, dtype=np.float64)
+        full_mass = bool(np.any(cov_p - np.diag(np.diag(cov_p))))
+        diag = t.diagonal and not full_mass
+        kind = H.HMC_TARGET_DIAG if diag else H.HMC_TARGET_DENSE
         q0 = None if t.zero_mean else _dev_tensor(t.q0, dev)
-        if t.diagonal:
+        if diag:
             prec = None if t.identity else _dev_tensor(np.diag(t.prec), dev)
         else:
             prec = _dev_tensor(t.prec, dev)
-        cov_p = np.asarray(self.cov_p, dtype=np.float64)
-        if np.any(cov_p - np.diag(np.diag(cov_p))):
-            raise NotImplementedError("non-diagonal cov_p: the GPU kernels support a diagonal mass matrix")
-        minv_d = np.diag(self.inv_cov_p).astype(np.float64)
-        ident_mass = np.all(np.diag(cov_p) == 1.0) and np.all(minv_d == 1.0)
-        minv = None if ident_mass else _dev_tensor(minv_d, dev)
-        pscale = None if ident_mass else _dev_tensor(np.sqrt(np.diag(cov_p)), dev)
+        minv_full = None
+        if full_mass:                     # samplers.py:356, :835-837 with a full inv_cov_p
+            minv = pscale = None
+            minv_full = _dev_tensor(self.inv_cov_p, dev)
+        else:
+            minv_d = np.diag(self.inv_cov_p).astype(np.float64)
+            ident_mass = np.all(np.diag(cov_p) == 1.0) and np.all(minv_d == 1.0)
+            minv = None if ident_mass else _dev_tensor(minv_d, dev)
+            pscale = None if ident_mass else _dev_tensor(np.sqrt(np.diag(cov_p)), dev)
         dt = np.asarray(self.dt, dtype=np.float64)
         if dt.ndim == 0:
             dtv, dts = None, float(dt)
         else:
             assert dt.size == self.D
             dtv, dts = _dev_tensor(dt.reshape(-1), dev), 0.0
-        keep += [q0, prec, minv, pscale, dtv]
+        kick = None if minv_full is None else _dev_tensor(self.inv_cov_p @ np.asarray(t.prec, np.float64), dev)
+        keep += [q0, prec, minv, pscale, dtv, minv_full, kick]
         T = H.Target(self.D, kind, H.ptr(q0), H.ptr(prec), t.logdet_const)
-        K = H.Kinetic(H.ptr(minv), H.ptr(pscale), H.ptr(dtv), dts)
+        K = H.Kinetic(H.ptr(minv), H.ptr(pscale), H.ptr(dtv), dts, H.ptr(minv_full), None, H.ptr(kick))
         return T, K, keep
 
     # ------------------------------------------------------------------ public API
