@@ -28,9 +28,10 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t k) {
   return r;
 }
 
-__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+template <int ROUNDS>
+__device__ __forceinline__ uint4 philox_rounds(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < ROUNDS; ++r) {
     // one v_mad_u64_u32 per 32x32->64 product (lo and hi words together), one v_bitop3 per xor pair
     const uint64_t p0 = (uint64_t)c.x * 0xD2511F53u;
     const uint64_t p1 = (uint64_t)c.z * 0xCD9E8D57u;
@@ -44,6 +45,8 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1
   return c;
 }
 
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) { return philox_rounds<10>(c, k0, k1); }
+
 // Loop-invariant value made opaque to the optimiser at its point of use (keeps a hoisted
 // first Philox round of every draw slot from occupying registers across a whole loop).
 __device__ __forceinline__ uint32_t opaque_u32(uint32_t v) {
@@ -54,6 +57,26 @@ __device__ __forceinline__ uint32_t opaque_u32(uint32_t v) {
 __device__ __forceinline__ uint4 draw_block(uint32_t slot, uint32_t iter, uint64_t gchain, uint32_t k0,
                                             uint32_t k1) {
   return philox4x32_10(make_uint4(slot, iter, (uint32_t)gchain, (uint32_t)(gchain >> 32)), k0, k1);
+}
+
+// draw_block when the chain (counter words z, w) is wave-uniform, as in the one-chain-per-wave
+// kernel: the first two rounds are written out so the products and xors of uniform words run on
+// the SALU (the asm xor3 of the generic round takes one SGPR operand only).  Same function.
+__device__ __forceinline__ uint4 draw_block_uc(uint32_t slot, uint32_t iter, uint64_t gchain, uint32_t k0,
+                                               uint32_t k1) {
+  const uint32_t glo = (uint32_t)gchain, ghi = (uint32_t)(gchain >> 32);
+  const uint64_t p0 = (uint64_t)slot * 0xD2511F53u;
+  const uint64_t p1 = (uint64_t)glo * 0xCD9E8D57u;                      // uniform
+  uint4 c = make_uint4(iter ^ ((uint32_t)(p1 >> 32) ^ k0), (uint32_t)p1, (uint32_t)(p0 >> 32) ^ (ghi ^ k1),
+                       (uint32_t)p0);
+  k0 += 0x9E3779B9u;
+  k1 += 0xBB67AE85u;
+  const uint64_t r0 = (uint64_t)c.x * 0xD2511F53u;
+  const uint64_t r1 = (uint64_t)c.z * 0xCD9E8D57u;
+  c = make_uint4((uint32_t)(r1 >> 32) ^ (c.y ^ k0), (uint32_t)r1, xor3((uint32_t)(r0 >> 32), c.w, k1), (uint32_t)r0);
+  k0 += 0x9E3779B9u;
+  k1 += 0xBB67AE85u;
+  return philox_rounds<8>(c, k0, k1);
 }
 
 // 53-bit uniform in [0, 1) from two words.
@@ -170,18 +193,24 @@ __device__ __forceinline__ void normal_pair(uint4 r, double& z0, double& z1) {
 
 // ---- table-driven Box–Muller (the wave kernel's momentum draws).  Per block, two small LDS
 // tables built once with the ~1-ulp kernels above:
-//   trig[i] = (cos, sin)(2*pi*i/256), i < 256            (4 KB)
-//   logt[j] = (1/c_j, -log(1/c_j)), c_j = centre of the j-th of 128 buckets of [0.5, 1)
+//   trig[i] = (cos, sin)(2*pi*i/1024), i < 1024          (16 KB)
+//   logt[j] = (1/c_j, -log(1/c_j)), c_j = centre of the j-th of 1024 buckets of [0.5, 1)
 //             (the last bucket uses c = 1: log is then log1p(m - 1), relative-accurate near 1)
-// so that log and sincos reduce to short Horner chains around a table point.
+// so that log and sincos reduce to short Horner chains around a table point (1024 entries: two
+// fewer terms in each series than 256/128 entries, for 16 KB more LDS per block).
+#ifdef HMC_SMALL_TABLES
 constexpr int kTrigN = 256, kLogN = 128;
+#else
+constexpr int kTrigN = 1024, kLogN = 1024;
+#endif
+constexpr int kLogShift = kLogN == 1024 ? 10 : 13, kTrigShift = kTrigN == 1024 ? 10 : 12;
 constexpr int kNormalTableDoubles = 2 * kTrigN + 2 * kLogN;
 
 // Every thread of the block calls this, then the block synchronises.
 __device__ __forceinline__ void init_normal_tables(double* tab) {
   for (int i = threadIdx.x; i < kTrigN; i += blockDim.x) {
     double sn, cs;
-    fast_sincospi((double)i * (1.0 / 128.0), sn, cs);
+    fast_sincospi((double)i * (2.0 / kTrigN), sn, cs);
     tab[2 * i] = cs;
     tab[2 * i + 1] = sn;
   }
@@ -195,18 +224,22 @@ __device__ __forceinline__ void init_normal_tables(double* tab) {
 
 __device__ __forceinline__ double2 lds_pair(const double* p) { return *reinterpret_cast<const double2*>(p); }
 
-// log(u) for u in (0, 1] from the tables: u = 2^k m, m in [0.5, 1); bucket j = top 7 mantissa
-// bits; log m = L_j + log1p(m / c_j - 1) with |r| <= 2^-8 (series to r^7).
+// log(u) for u in (0, 1] from the tables: u = 2^k m, m in [0.5, 1); bucket j = top 10 mantissa
+// bits; log m = L_j + log1p(m / c_j - 1) with |r| <= 2^-11 (series to r^5; r^6/6 < 2^-68).
 __device__ __forceinline__ double table_log(double u, const double* tab) {
   const int k = __builtin_amdgcn_frexp_exp(u);
   const double m = __builtin_amdgcn_frexp_mant(u);
   const uint32_t mhi = (uint32_t)(__builtin_bit_cast(uint64_t, m) >> 32);
-  const int j = (int)((mhi >> 13) & (kLogN - 1));
+  const int j = (int)((mhi >> kLogShift) & (kLogN - 1));
   const double2 e = lds_pair(tab + 2 * kTrigN + 2 * j);
   const double r = __builtin_fma(m, e.x, -1.0);
+#ifdef HMC_SMALL_TABLES
   double pl = fmac_k(r, 1.0 / 7.0, -1.0 / 6.0);
   pl = fmac_k(r, pl, 1.0 / 5.0);
   pl = fmac_k(r, pl, -1.0 / 4.0);
+#else
+  double pl = fmac_k(r, 1.0 / 5.0, -1.0 / 4.0);
+#endif
   pl = fmac_k(r, pl, 1.0 / 3.0);
   pl = fmac_k(r, pl, -0.5);
   const double l1p = __builtin_fma(r * r, pl, r);                       // log1p(r)
@@ -215,20 +248,28 @@ __device__ __forceinline__ double table_log(double u, const double* tab) {
 }
 
 // (cos, sin)(2*pi*(d - 1)) for d in [1, 2) holding 52 random mantissa bits: table point from the
-// top 8 bits, the rest delta in [0, 2*pi/256) by Taylor series (to delta^8).
+// top 10 bits, the rest delta in [0, 2*pi/1024) by Taylor series (sin to delta^5, cos to delta^6:
+// the next terms are below 2^-60 relative).
 __device__ __forceinline__ void table_cossin(double d, const double* tab, double& cs, double& sn) {
   const uint64_t bits = __builtin_bit_cast(uint64_t, d);
   const uint32_t hi = (uint32_t)(bits >> 32);
-  const int i = (int)((hi >> 12) & (kTrigN - 1));
-  const double f = __builtin_bit_cast(double, bits & ~(0xFFull << 44)) - 1.0;    // [0, 2^-8), exact
+  const int i = (int)((hi >> kTrigShift) & (kTrigN - 1));
+  const double f = __builtin_bit_cast(double, bits & ~((uint64_t)(kTrigN - 1) << (32 + kTrigShift))) - 1.0;  // exact
   const double dl = __builtin_fma(f, 6.28318530717958623200e+00, f * 2.44929359829470635445e-16);
   const double z = dl * dl;
+#ifdef HMC_SMALL_TABLES
   double ps = fmac_k(z, -1.0 / 5040.0, 1.0 / 120.0);
   ps = fmac_k(z, ps, -1.0 / 6.0);
   const double sd = __builtin_fma(dl * z, ps, dl);                       // sin(delta)
   double pc = fmac_k(z, 1.0 / 40320.0, -1.0 / 720.0);
   pc = fmac_k(z, pc, 1.0 / 24.0);
   pc = fmac_k(z, pc, -0.5);
+#else
+  const double ps = fmac_k(z, 1.0 / 120.0, -1.0 / 6.0);
+  const double sd = __builtin_fma(dl * z, ps, dl);                       // sin(delta)
+  double pc = fmac_k(z, -1.0 / 720.0, 1.0 / 24.0);
+  pc = fmac_k(z, pc, -0.5);
+#endif
   const double cd = __builtin_fma(z, pc, 1.0);                          // cos(delta)
   const double2 t = lds_pair(tab + 2 * i);                              // (cos, sin)(theta_i)
   cs = __builtin_fma(t.x, cd, -(t.y * sd));
@@ -329,15 +370,24 @@ __device__ __forceinline__ double dpp_u(double v) {
   return __hiloint2double(hi, lo);
 }
 
-__device__ __forceinline__ double wave_sum_dpp(double v) {
+// The DPP chain alone: lane 63 holds the full-wave sum, other lanes partial sums.  Callers that
+// only compare the total (the Metropolis test) finish the arithmetic in lane 63 and read the
+// decision from the compare mask, with no readlane / v_mov round trip.
+__device__ __forceinline__ double wave_sum_dpp_l63(double v) {
   v += dpp_u<0x111>(v);        // row_shr:1 (bound_ctrl: lanes shifted in from outside the row read 0)
   v += dpp_u<0x112>(v);        // row_shr:2
   v += dpp_u<0x114>(v);        // row_shr:4
   v += dpp_u<0x118>(v);        // row_shr:8
   v += dpp_u<0x142, 0xA>(v);   // row_bcast:15 -> rows 1, 3
   v += dpp_u<0x143, 0xC>(v);   // row_bcast:31 -> rows 2, 3
-  return readlane_d(v, 63);
+  return v;
 }
+
+__device__ __forceinline__ double wave_sum_dpp(double v) { return readlane_d(wave_sum_dpp_l63(v), 63); }
+
+// Lane 63's bit of a compare mask as a wave-uniform bool (EXEC must be all ones): the sign of the
+// mask's high word, tested on the SALU.
+__device__ __forceinline__ bool lane63(uint64_t mask) { return (int32_t)(uint32_t)(mask >> 32) < 0; }
 
 __device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ double uniform_d(double v) { return readlane_d(v, 0); }

@@ -42,6 +42,23 @@ __device__ __forceinline__ void wave_partials(const RandArgs& a, const int (&kk)
   }
 }
 
+// FAST (non-EXACT) diagonal-identity partials as FMA chains: x.x and x.x + p.p of this lane's
+// coordinates (the reference sums V and K separately; FAST only promises agreement to 1e-10).
+template <int K>
+__device__ __forceinline__ void wave_partials_fma(const double (&q)[2 * K], const double (&p)[2 * K], double& maha,
+                                                  double& tot) {
+  maha = q[1] * q[1];
+  maha = __builtin_fma(q[0], q[0], maha);
+#pragma unroll
+  for (int j = 1; j < K; ++j) {
+    maha = __builtin_fma(q[2 * j], q[2 * j], maha);
+    maha = __builtin_fma(q[2 * j + 1], q[2 * j + 1], maha);
+  }
+  tot = maha;
+#pragma unroll
+  for (int e = 0; e < 2 * K; ++e) tot = __builtin_fma(p[e], p[e], tot);
+}
+
 template <int K, bool GEN>
 __device__ __forceinline__ double kin_partial(const RandArgs& a, const int (&kk)[K], const bool (&pv)[K],
                                               const double (&p)[2 * K]) {
@@ -106,7 +123,9 @@ constexpr int kRingPairs = 128;
 // variant (FULL = false) drops them: their pointers and flags are live across the iteration loop
 // and pushed the SGPR demand past the 8-waves/SIMD budget (spills to VGPR lanes cost one
 // v_readlane/v_writelane VALU slot each, ~45 per iteration).
-template <int K, bool EXACT, bool GEN, bool REPLAY, bool FULL>
+// ODD: D is odd (the ring zeroes the missing coordinate of the last pair); a template parameter so
+// that the common even-D kernel carries no per-pass test.
+template <int K, bool EXACT, bool GEN, bool REPLAY, bool FULL, bool ODD = false>
 __device__ __forceinline__ void wave_iters(const RandArgs& a) {
 #ifdef HMC_NO_RING
   constexpr bool RING = false;
@@ -114,7 +133,8 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
   constexpr bool RING = K == 1 && !REPLAY;
 #endif
   __shared__ double s_ntab[REPLAY ? 2 : kNormalTableDoubles];   // Box–Muller tables (Philox mode)
-  __shared__ double s_ring[RING ? (kK1Block / kWave) * 2 * kRingPairs : 2];
+  // per wave: kRingPairs ring slots + one zero pair that lanes past npairs read (p = 0 there)
+  __shared__ double s_ring[RING ? (kK1Block / kWave) * 2 * (kRingPairs + 1) : 2];
   if constexpr (!REPLAY) {
     init_normal_tables(s_ntab);
     __syncthreads();
@@ -123,41 +143,47 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
   const int64_t c = uniform_i(blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave));
   if (c >= a.n) return;                                  // whole wave, uniform
   const uint64_t gc = (uint64_t)(a.chain_offset + c);
-  double* const ring = s_ring + (RING ? (threadIdx.x / kWave) * 2 * kRingPairs : 0);
-  int gen_n = 0, gen_it = a.it0, gen_k = 0;              // pairs drawn so far; (iteration, pair) of the next
+  double* const ring = s_ring + (RING ? (threadIdx.x / kWave) * 2 * (kRingPairs + 1) : 0);
+  if constexpr (RING) {
+    if (lane == 0) *reinterpret_cast<double2*>(ring + 2 * kRingPairs) = make_double2(0.0, 0.0);
+  }
+  // Generator position: pairs drawn so far (wave-uniform) and this lane's (pair, iteration) for the
+  // next pass.  npairs is in (32, 64] for the wave kernel, so one pass of 64 pairs advances a lane
+  // by one or two whole iterations: the position is kept incrementally instead of re-derived.
+  int gen_n = 0;
+  int gk = lane, git = a.it0;
+  if (gk >= a.npairs) { gk -= a.npairs; ++git; }
   // momentum of iteration `it` through the ring: at most one 64-pair pass is due (the pairs drawn
   // so far cover every earlier iteration and npairs <= 64), and the ring never holds more than
   // npairs + 64 <= kRingPairs pairs that are not consumed yet
   auto ring_momentum = [&](int it, double (&pp)[2 * K]) {
     const int base = (it - a.it0) * a.npairs;
     if (gen_n < base + a.npairs) {                       // wave-uniform
-      int k = gen_k + lane, itl = gen_it;
-      if (k >= a.npairs) { k -= a.npairs; ++itl; }
-      if (k >= a.npairs) { k -= a.npairs; ++itl; }
       double z0, z1;
-      normal_pair_tab(draw_block((uint32_t)k, (uint32_t)itl, gc, a.k0, a.k1), s_ntab, z0, z1);
+      normal_pair_tab(draw_block((uint32_t)gk, (uint32_t)git, gc, a.k0, a.k1), s_ntab, z0, z1);
+      if constexpr (ODD) z1 = gk == a.npairs - 1 ? 0.0 : z1;   // dimension D does not exist
       *reinterpret_cast<double2*>(ring + 2 * ((gen_n + lane) & (kRingPairs - 1))) = make_double2(z0, z1);
       __builtin_amdgcn_wave_barrier();
       gen_n += kWave;
-      gen_k += kWave;
-      while (gen_k >= a.npairs) {
-        gen_k -= a.npairs;
-        ++gen_it;
-      }
+      gk += kWave - a.npairs;                            // >= 0: one wrap always happens
+      const int wrap = gk >= a.npairs ? 1 : 0;           // and at most one more
+      git += 1 + wrap;
+      gk -= wrap * a.npairs;
     }
-    pp[0] = pp[1] = 0.0;
-    if (lane < a.npairs) {
-      const double2 z = *reinterpret_cast<const double2*>(ring + 2 * ((base + lane) & (kRingPairs - 1)));
+    // lanes past npairs read the zero pair: p = 0 in the padding without a branch
+    const int slot = lane < a.npairs ? ((base + lane) & (kRingPairs - 1)) : kRingPairs;
+    const double2 z = *reinterpret_cast<const double2*>(ring + 2 * slot);
+    pp[0] = z.x;
+    pp[1] = z.y;
+    if (GEN && a.pscale && lane < a.npairs) {
       const int d = 2 * lane;
-      pp[0] = z.x;
-      pp[1] = d + 1 < a.D ? z.y : 0.0;
-      if (GEN && a.pscale) {
-        pp[0] *= a.pscale[d];
-        if (d + 1 < a.D) pp[1] *= a.pscale[d + 1];
-      }
+      pp[0] *= a.pscale[d];
+      if (d + 1 < a.D) pp[1] *= a.pscale[d + 1];
     }
   };
-  const bool even = (a.D & 1) == 0;
+  // the ring (Philox, K = 1) kernels are specialised on the parity of D: `even` is then a
+  // compile-time constant and the row stores need no masks (SGPR pressure: no spilled flags)
+  const bool even = RING ? !ODD : (a.D & 1) == 0;
   int kk[K];
   bool pv[K];
   double q[2 * K], p[2 * K], qi[2 * K], pn[2 * K];
@@ -175,16 +201,26 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
   // momentum and energy of the first iteration of this launch
   if constexpr (RING) ring_momentum(a.it0, p);
   else wave_momentum<K, GEN, REPLAY>(a, c, gc, a.it0, kk, pv, p, s_ntab);
+  // FASTID: FAST integrator on an identity-precision target (the headline instantiation): FMA
+  // energy partials, E = fma(sum, 1/2, logc/2), Metropolis test finished in lane 63
+  constexpr bool FASTID = !EXACT && !GEN;
+  const double hlogc = 0.5 * a.logc;
   double m0, k0, m0l;   // m0l: this lane's part of the potential of q (FAST mode bookkeeping)
-  wave_partials<K, GEN>(a, kk, pv, q, p, m0, k0);
-  m0l = m0;
+  if constexpr (FASTID) {
+    wave_partials_fma<K>(q, p, m0l, k0);
+    m0 = m0l;
+  } else {
+    wave_partials<K, GEN>(a, kk, pv, q, p, m0, k0);
+    m0l = m0;
+  }
   if constexpr (EXACT) {   // reference grouping: V and K summed separately
     m0 = wave_sum_dpp(m0);
     k0 = wave_sum_dpp(k0);
-  } else {                 // one reduction of V + K
+  } else if constexpr (!FASTID) {   // one reduction of V + K
     k0 = wave_sum_dpp(m0 + k0);
   }
-  double E0 = EXACT ? 0.5 * (a.logc + (m0 + k0)) : 0.5 * (a.logc + k0);
+  double E0 = EXACT ? 0.5 * (a.logc + (m0 + k0))
+                    : (FASTID ? __builtin_fma(wave_sum_dpp(k0), 0.5, hlogc) : 0.5 * (a.logc + k0));
 
   // thinning bookkeeping without divisions: row = (it - wu)//thin, phase = (it - wu) % thin
   int row = 0, phase = 0;
@@ -193,11 +229,23 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     phase = (a.it0 - a.wu) - row * a.thin;
   }
   int qslot = row % a.Lq;                                // q_chain buffer row of `row` (circular window)
-  double Ebuf = 0.0, dEbuf = 0.0;
-  int rowbuf = -1, nbuf = 0;
+  double Ebuf = 0.0, dEbuf = 0.0, Eprev_first = 0.0;
+  int row_first = 0, nbuf = 0;
+  const bool thin1 = a.thin == 1;
   double* const Ec = a.Ec ? a.Ec + c * (int64_t)a.Lc : nullptr;
   double* const dEc = a.dEc ? a.dEc + c * (int64_t)a.Lc : nullptr;
   double* const qcb = a.qc ? a.qc + c * (int64_t)a.Lq * a.D : nullptr;
+  auto flush_E = [&](int n) {          // rows row_first .. row_first + n - 1 from lanes 0 .. n-1
+    double dE = dEbuf;
+    if (thin1) {
+      const double before = __shfl_up(Ebuf, 1, kWave);
+      dE = Ebuf - (lane == 0 ? Eprev_first : before);
+    }
+    if (lane < n) {
+      if (Ec) __builtin_nontemporal_store(Ebuf, Ec + row_first + lane);
+      if (dEc) __builtin_nontemporal_store(dE, dEc + row_first + lane);
+    }
+  };
   const bool cap_chain = FULL && a.traj_q && gc == 0 && !(a.dbg & 32);
   // per-launch tallies of one chain: (it1 - it0) <= 2^31 / L_high^2 is checked on the host, so
   // 32-bit counters cannot wrap (half the SGPRs of 64-bit ones)
@@ -208,19 +256,28 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
   for (int it = a.it0; it < a.it1; ++it) {
     const bool post = it >= a.wu;
     const bool write_row = post && ((it == a.niter) || (phase == a.thin - 1));
-    // E_chain / dE_chain of this iteration parked in lane nbuf (flushed every 64 or at the end)
+    // E_chain / dE_chain of this iteration parked in lane nbuf (flushed every 64 or at the end).
+    // Parked rows are consecutive (row_first + lane).  With thin = 1 they are also consecutive
+    // iterations, so dE = E(lane) - E(lane - 1) is formed at the flush (lane 0: the E before the
+    // block) and only E is parked; otherwise dE is parked too.
+    // (the empty asm statements keep these uniform conditions as branches, not per-lane selects)
     if (write_row) {
-      if (lane == nbuf) {
-        Ebuf = E0;
-        dEbuf = E0 - Eprev;
-        rowbuf = row;
+      if (nbuf == 0) {
+        asm volatile("" ::: "memory");
+        row_first = row;
+        Eprev_first = Eprev;
+      }
+      if (thin1) {
+        if (lane == nbuf) Ebuf = E0;
+      } else {
+        asm volatile("" ::: "memory");
+        if (lane == nbuf) {
+          Ebuf = E0;
+          dEbuf = E0 - Eprev;
+        }
       }
       if (++nbuf == kWave) {
-        if (rowbuf >= 0) {
-          if (Ec) __builtin_nontemporal_store(Ebuf, Ec + rowbuf);
-          if (dEc) __builtin_nontemporal_store(dEbuf, dEc + rowbuf);
-        }
-        rowbuf = -1;
+        flush_E(kWave);
         nbuf = 0;
       }
     }
@@ -337,22 +394,45 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     if (more && !(FULL && (a.dbg & 256))) {
       if constexpr (RING) ring_momentum(it + 1, pn);
       else wave_momentum<K, GEN, REPLAY>(a, c, gc, it + 1, kk, pv, pn, s_ntab);
-      kn = kin_partial<K, GEN>(a, kk, pv, pn);
+      if constexpr (FASTID) {
+        kn = pn[1] * pn[1];
+        kn = __builtin_fma(pn[0], pn[0], kn);
+#pragma unroll
+        for (int e = 2; e < 2 * K; ++e) kn = __builtin_fma(pn[e], pn[e], kn);
+      } else {
+        kn = kin_partial<K, GEN>(a, kk, pv, pn);
+      }
     }
     double m1, k1, m1l;
-    wave_partials<K, GEN>(a, kk, pv, q, p, m1, k1);
-    m1l = m1;
-    if constexpr (EXACT) {
-      m1 = wave_sum_dpp(m1);
-      k1 = wave_sum_dpp(k1);
-      kn = wave_sum_dpp(kn);
+    bool accept;
+    if constexpr (FASTID) {
+      wave_partials_fma<K>(q, p, m1l, k1);
+      m1 = m1l;
+      // E1 - E0 and the test in lane 63, where the DPP chain leaves the total (samplers.py:459-462)
+      const double dE = __builtin_fma(wave_sum_dpp_l63(k1), 0.5, hlogc) - E0;
+#ifdef HMC_AB_SELECT
+      accept = __builtin_amdgcn_ballot_w64((dE < 0.0) || (lnu < -dE)) >> 63;
+#else
+      accept = lane63(__builtin_amdgcn_ballot_w64(dE < 0.0) | __builtin_amdgcn_ballot_w64(lnu < -dE));
+#endif
     } else {
-      k1 = wave_sum_dpp(m1 + k1);
+      wave_partials<K, GEN>(a, kk, pv, q, p, m1, k1);
+      m1l = m1;
+      if constexpr (EXACT) {
+        m1 = wave_sum_dpp(m1);
+        k1 = wave_sum_dpp(k1);
+        kn = wave_sum_dpp(kn);
+      } else {
+        k1 = wave_sum_dpp(m1 + k1);
+      }
+      const double E1 = EXACT ? 0.5 * (a.logc + (m1 + k1)) : 0.5 * (a.logc + k1);
+      const double dE = E1 - E0;                          // samplers.py:459
+      accept = (dE < 0.0) || (lnu < -dE);                 // :462
     }
-    const double E1 = EXACT ? 0.5 * (a.logc + (m1 + k1)) : 0.5 * (a.logc + k1);
-    const double dE = E1 - E0;                            // samplers.py:459
-    const bool accept = (dE < 0.0) || (lnu < -dE);        // :462
     if (!accept && !(FULL && (a.dbg & 128))) {
+#ifndef HMC_AB_SELECT
+      asm volatile("" ::: "memory");   // keep a (uniform) branch: no per-iteration selects on accept
+#endif
 #pragma unroll
       for (int e = 0; e < 2 * K; ++e) q[e] = qi[e];
     }
@@ -360,7 +440,7 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
       double* rowp = qcb + (int64_t)qslot * a.D;
 #pragma unroll
       for (int j = 0; j < K; ++j)
-        if (pv[j]) store_pair_nt(rowp, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);
+        if (pv[j]) store_pair_nt(rowp, kk[j], even, even || 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);
     }
     if (cap && lane == 0) {
       a.traj_len[it - 1] = (L > 0 ? L : 0) + 1;
@@ -382,8 +462,13 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
         m0 = accept ? m1 : m0;
         E0 = 0.5 * (a.logc + (m0 + kn));
       } else {                                            // V(q_next) + K(p_next) in one reduction
-        m0l = accept ? m1l : m0l;
-        E0 = 0.5 * (a.logc + wave_sum_dpp(m0l + kn));
+        if (accept) {
+#ifndef HMC_AB_SELECT
+          asm volatile("" ::: "memory");
+#endif
+          m0l = m1l;
+        }
+        E0 = FASTID ? __builtin_fma(wave_sum_dpp(m0l + kn), 0.5, hlogc) : 0.5 * (a.logc + wave_sum_dpp(m0l + kn));
       }
     }
     if (post && ++phase == a.thin) {
@@ -394,10 +479,7 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
   }
 
   // flush parked E/dE, write back state and counters
-  if (rowbuf >= 0) {
-    if (Ec) __builtin_nontemporal_store(Ebuf, Ec + rowbuf);
-    if (dEc) __builtin_nontemporal_store(dEbuf, dEc + rowbuf);
-  }
+  if (nbuf > 0) flush_E(nbuf);
 #pragma unroll
   for (int j = 0; j < K; ++j)
     if (pv[j]) store_pair(qrow, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);
@@ -421,9 +503,9 @@ __global__ __launch_bounds__(256) void k_wave_iters(RandArgs a) {
   wave_iters<K, EXACT, GEN, REPLAY, FULL>(a);
 }
 
-template <bool EXACT, bool GEN, bool REPLAY, bool FULL>
+template <bool EXACT, bool GEN, bool REPLAY, bool FULL, bool ODD>
 __global__ __launch_bounds__(kK1Block) __attribute__((amdgpu_waves_per_eu(8))) void k_wave_iters_k1(RandArgs a) {
-  wave_iters<1, EXACT, GEN, REPLAY, FULL>(a);
+  wave_iters<1, EXACT, GEN, REPLAY, FULL, ODD>(a);
 }
 
 template <int K, bool EXACT, bool GEN, bool REPLAY>
@@ -431,8 +513,14 @@ void launch_wave_one(const RandArgs& a, dim3 grid, hipStream_t s) {
   const bool full = a.traj_q != nullptr || a.dbg != 0 || a.dbgL >= 0;
   if constexpr (K == 1) {
     const dim3 g1((unsigned)((a.n + kK1Block / kWave - 1) / (kK1Block / kWave)));
-    if (full) k_wave_iters_k1<EXACT, GEN, REPLAY, true><<<g1, kK1Block, 0, s>>>(a);
-    else k_wave_iters_k1<EXACT, GEN, REPLAY, false><<<g1, kK1Block, 0, s>>>(a);
+    const bool odd = (a.D & 1) != 0 && !REPLAY;   // only the ring (Philox) path specialises on odd D
+    if (full) {
+      if (odd) k_wave_iters_k1<EXACT, GEN, REPLAY, true, !REPLAY><<<g1, kK1Block, 0, s>>>(a);
+      else k_wave_iters_k1<EXACT, GEN, REPLAY, true, false><<<g1, kK1Block, 0, s>>>(a);
+    } else {
+      if (odd) k_wave_iters_k1<EXACT, GEN, REPLAY, false, !REPLAY><<<g1, kK1Block, 0, s>>>(a);
+      else k_wave_iters_k1<EXACT, GEN, REPLAY, false, false><<<g1, kK1Block, 0, s>>>(a);
+    }
   } else {
     if (full) k_wave_iters<K, EXACT, GEN, REPLAY, true><<<grid, 256, 0, s>>>(a);
     else k_wave_iters<K, EXACT, GEN, REPLAY, false><<<grid, 256, 0, s>>>(a);
