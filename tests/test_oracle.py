@@ -158,3 +158,24 @@ def test_tree_tables_vs_reference_and_readme():
                 if l > 1 and O.release_fast(m, l):
                     table[s] = -1
     assert lines == t["flatten_print"]
+
+
+def test_nuts_closed_form_save_slots():
+    """hmc_nuts.hip keeps saved odd point l of a sub-tree in slot ctz(l - 1) (point 1: slot
+    d_max) instead of the reference's searched table (utils.py:222-385): every point that
+    check_points(m) names must still be in its slot when m is reached, for every sub-tree size
+    the reference can build (d < d_max <= 15)."""
+    from hmc_amd.utils import check_points
+
+    def slot(l, d_max):
+        return d_max if l == 1 else ((l - 1) & -(l - 1)).bit_length() - 1
+    for d_max in range(1, 16):
+        for d in range(d_max):
+            held = {}
+            for m in range(1, (1 << d) + 1):
+                if m % 2:
+                    assert 0 <= slot(m, d_max) <= d_max
+                    held[slot(m, d_max)] = m
+                else:
+                    for l in check_points(m):
+                        assert held.get(slot(int(l), d_max)) == int(l), (d_max, d, m, l)

@@ -11,10 +11,24 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int kDenseWaves = 4;   // waves per block: one block per CU (one P copy in LDS), one wave per SIMD with the full 512-register file
 
+// Sum over lanes c, c+16, c+32, c+48 with gfx950's row swaps (v_permlane16_swap /
+// v_permlane32_swap: VALU lane exchanges, no LDS round trip).  Swapping a register with itself
+// leaves, in the two results, each lane's own value and its xor-16 (xor-32) partner in some order,
+// so r0 + r1 is v[l] + v[l ^ 16] (then ^ 32): the same two-level sum as shuffles, bit for bit.
+__device__ __forceinline__ double xor_sum_16(double v) {
+  const unsigned lo = __double2loint(v), hi = __double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+}
+__device__ __forceinline__ double xor_sum_32(double v) {
+  const unsigned lo = __double2loint(v), hi = __double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+}
 __device__ __forceinline__ double chain_sum4(double v) {   // sum over lanes c, c+16, c+32, c+48
-  v += __shfl_xor(v, 16, kWave);
-  v += __shfl_xor(v, 32, kWave);
-  return v;
+  return xor_sum_32(xor_sum_16(v));
 }
 
 typedef __attribute__((address_space(3))) const double lds_cf64;

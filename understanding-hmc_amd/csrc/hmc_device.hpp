@@ -390,6 +390,22 @@ __device__ __forceinline__ double wave_sum_dpp(double v) { return readlane_d(wav
 __device__ __forceinline__ bool lane63(uint64_t mask) { return (int32_t)(uint32_t)(mask >> 32) < 0; }
 
 __device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Wave-uniform max of an int: DPP row_shr 1/2/4/8 then row_bcast 15/31 (each step one VALU max
+// with the DPP source; lanes without a source keep their value), lane 63 read back.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ int dpp_max_step(int v) {
+  return max(v, __builtin_amdgcn_update_dpp(v, v, CTRL, ROW_MASK, 0xF, false));
+}
+__device__ __forceinline__ int wave_max_i32(int v) {
+  v = dpp_max_step<0x111>(v);
+  v = dpp_max_step<0x112>(v);
+  v = dpp_max_step<0x114>(v);
+  v = dpp_max_step<0x118>(v);
+  v = dpp_max_step<0x142, 0xA>(v);
+  v = dpp_max_step<0x143, 0xC>(v);
+  return __builtin_amdgcn_readlane(v, 63);
+}
 __device__ __forceinline__ double uniform_d(double v) { return readlane_d(v, 0); }
 
 }  // namespace hmc

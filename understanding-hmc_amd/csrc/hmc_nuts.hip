@@ -27,11 +27,23 @@ namespace {
 
 constexpr int kMaxDepth = 16;   // table size bound (d_max <= 15)
 
+// Waves per block (one block per CU: the LDS copy of P), one per SIMD with the whole register file.
+// 8 (two waves per SIMD, 256 registers each) was measured at 0.42x: the step spills ~560 B per lane
+// to scratch and the queue's tail grows (lane utilisation 0.80 -> 0.66).
+#ifndef HMC_NUTS_WAVES
+#define HMC_NUTS_WAVES 4
+#endif
+constexpr int kNutsWaves = HMC_NUTS_WAVES;
+
 // S_FETCH: the chain slot takes the next chain of the launch from the queue (or retires);
 // S_GRAD: a fetched chain waits one wave step for the MFMA gradient at its start point.
-enum : int { S_ITER_START = 0, S_SUB_START = 1, S_READY = 2, S_ITER_END = 3, S_DONE = 4, S_FETCH = 5, S_GRAD = 6 };
+// S_SUB_LOAD: a doubling in the direction opposite to the last sub-tree loads that end first.
+enum : int { S_ITER_START = 0, S_SUB_START = 1, S_READY = 2, S_ITER_END = 3, S_DONE = 4, S_FETCH = 5, S_GRAD = 6,
+             S_SUB_LOAD = 7 };
 
-// workspace vector ids (per chain)
+// workspace vector ids (per chain).  The live points old/new (:577, :623, :750, :775) are two
+// buffer pairs, (0, 1) and (2, 3): `old2` (0 or 2, per chain) names the old pair and the other is
+// new, so accepting a sub-tree's point swaps the names instead of copying two vectors.
 enum : int { V_OLD_Q = 0, V_OLD_G = 1, V_NEW_Q = 2, V_NEW_G = 3, V_LEFT_Q = 4, V_LEFT_P = 5, V_LEFT_G = 6,
              V_RIGHT_Q = 7, V_RIGHT_P = 8, V_RIGHT_G = 9, V_SLOTS = 10 };
 
@@ -115,6 +127,15 @@ __device__ __forceinline__ void gload(const WaveWS& w, int v, int vl, d4 (&acc)[
   }
 }
 
+// Save slot of odd point l of a sub-tree.  The reference keeps the saved odd points in a table
+// (find_next / retrieve_save_index / release_fast, utils.py:222-385) and looks them up by value.
+// A saved point l is only ever checked as the first point of an aligned block of size s | (l - 1)
+// ending at an even point m <= l + lowbit(l - 1) - 1, so two points with the same level
+// ctz(l - 1) are never needed at the same time: slot = ctz(l - 1) (point 1, the start of every
+// block, gets slot d_max) holds exactly the points the table would hold when they are checked,
+// with no search and no releases.
+__device__ __forceinline__ int save_slot(int l, int d_max) { return l == 1 ? d_max : __builtin_ctz(l - 1); }
+
 // closed forms of utils.py check_points / release_fast (integer bit logic)
 __device__ __forceinline__ int cp_r(int m) {   // r of check_points(m): strip leading bits until pow2 or <= 2
   int r = m;
@@ -149,7 +170,8 @@ __device__ __forceinline__ double mac(double acc, double x, double y) {
 }
 
 template <int MT, bool EXACT, bool GEN, bool REPLAY>
-__global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
+__global__ __launch_bounds__(64 * kNutsWaves) __attribute__((amdgpu_waves_per_eu(kNutsWaves / 4, kNutsWaves / 4)))
+void k_nuts_iters(RandArgs a) {
   constexpr int M = 4 * MT;
   extern __shared__ double sP[];
   stage_precision<MT>(a, sP);
@@ -161,7 +183,7 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
   // next one.  Slots no longer idle while the slowest tree of a fixed 16-chain group finishes
   // (lane utilisation).  Draws are keyed by the chain, so results do not depend on which slot or
   // wave runs it.  The tree vectors are per slot (W), the tape cursors per chain.
-  const int64_t wv = (int64_t)blockIdx.x * kDenseWaves + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int64_t wv = (int64_t)blockIdx.x * kNutsWaves + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int64_t wave_doubles = (int64_t)nuts_nvec(a.d_max) * M * kWave;
   const int64_t n_waves = (a.n + 15) / 16;
   const WaveWS W{__builtin_amdgcn_make_buffer_rsrc(a.ws + wv * wave_doubles, 0, (int)(wave_doubles * 8), 0x00020000),
@@ -186,10 +208,8 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
   int d = 0, k = 0, Lsub = 1, udir = 0, ndraw = 0;
   bool lterm = false, rterm = false;
   double E_init = 0.0, E_max_now = 0.0, E_max_old = 0.0, pi_new = 1.0, pi_old = 1.0;
-  // save_index_table (:535) of this chain in LDS after P; the chain's 4 lanes keep identical copies
-  int* const table = reinterpret_cast<int*>(sP + MT * 4 * MT * kWave) +
-                     ((threadIdx.x / kWave) * 16 + (lane & 15)) * kMaxDepth;
   int64_t tpos = 0;                                     // replay tape cursor (persists across launches)
+  int old2 = 0;                                         // vector offset of the live_point_old pair
   unsigned long long n_lf = 0, n_unst = 0, n_dmax = 0, n_tape = 0, n_steps = 0;
 
   auto draw = [&](bool direction) -> double {           // next random number of this chain (reference order)
@@ -211,8 +231,8 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
     {
       const bool at_end = state == S_ITER_END;
       if (at_end) {                                     // samplers.py:786-791: q = live_point_q_old
-        vload<M>(W, V_OLD_Q, 0, q);
-        gload<MT>(W, V_OLD_G, 0, acc);
+        vload<M>(W, V_OLD_Q, old2, q);
+        gload<MT>(W, V_OLD_G, old2, acc);
         const int qrow = (it - a.wu) / a.thin;
         if (write_row_of(it) && a.qc && qrow >= a.q_row0) {
           double* rowp = a.qc + (c * (int64_t)a.Lq + qrow % a.Lq) * a.D;
@@ -268,6 +288,7 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
             kin += z * (dim_minv<MT, GEN>(a, h + 4 * m) * z);
             vput<M>(W, V_RIGHT_P, m, z);
             vput<M>(W, V_LEFT_P, m, -z);
+            p[m] = z;
           }
         } else {
 #pragma unroll
@@ -285,6 +306,8 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
             kin += z1 * (dim_minv<MT, GEN>(a, d1) * z1);
             vput2<M>(W, V_RIGHT_P, m, z0, z1);
             vput2<M>(W, V_LEFT_P, m, -z0, -z1);
+            p[m] = z0;
+            p[m + 1] = z1;
             __builtin_amdgcn_sched_barrier(0);
           }
         }
@@ -297,8 +320,8 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
           if (a.Ec) a.Ec[row] = E_init;
           if (a.dEc) a.dEc[row] = E_init - Eprev;
         }
-        vstore<M>(W, V_OLD_Q, 0, q);                    // live_point_q_old = q (:577)
-        gstore<MT>(W, V_OLD_G, 0, acc);
+        vstore<M>(W, V_OLD_Q, old2, q);                 // live_point_q_old = q (:577)
+        gstore<MT>(W, V_OLD_G, old2, acc);
         vstore<M>(W, V_LEFT_Q, 0, q);                   // left = (q, -p), right = (q, p) (:581-584)
         gstore<MT>(W, V_LEFT_G, 0, acc);
         vstore<M>(W, V_RIGHT_Q, 0, q);
@@ -310,10 +333,17 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
         ndraw = 0;
         state = S_SUB_START;
       }
-      if (state == S_SUB_START) {                       // one doubling (:595-626); d < d_max here
-        for (int i = 0; i <= a.d_max; ++i) table[i] = -1;
-        Lsub = 1 << d;
+      if (state == S_SUB_START) {                       // first doubling (:595-626) of an iteration
+        Lsub = 1;                                       // d = 0
         udir = (int)draw(true);                         // :608
+        if (udir != 0) {                                // both ends are (q, +-p): registers hold them
+#pragma unroll
+          for (int m = 0; m < M; ++m) p[m] = -p[m];
+        }
+        k = 0;
+        state = S_READY;
+      }
+      if (state == S_SUB_LOAD) {                        // a doubling towards the other end: load it
         const int b = udir == 0 ? V_RIGHT_Q : V_LEFT_Q;
         vload<M>(W, 0, b, q);
         vload<M>(W, 1, b, p);
@@ -377,14 +407,13 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
     const int mpt = k + 1;                              // point number within the sub-tree
     const bool first = act && k == 0, later = act && k > 0;
     if (first) {                                        // first point (:617-626)
-      vstore<M>(W, V_NEW_Q, 0, q);
-      gstore<MT>(W, V_NEW_G, 0, acc);
+      vstore<M>(W, V_OLD_Q, 2 - old2, q);               // live_point_new (the other buffer pair)
+      gstore<MT>(W, V_OLD_G, 2 - old2, acc);
       maha_new = maha_pt;
       E_max_now = E_tmp;
       pi_new = 1.0;
-      table[0] = 1;
-      vstore<M>(W, V_SLOTS, 0, q);
-      vstore<M>(W, V_SLOTS + 1, 0, p);
+      vstore<M>(W, V_SLOTS, 2 * a.d_max, q);            // point 1: save_slot(1)
+      vstore<M>(W, V_SLOTS + 1, 2 * a.d_max, p);
       k = 1;
       sub_end = Lsub == 1;
     } else if (later) {
@@ -392,9 +421,7 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
         reject = true;
         if (h == 0) ++n_unst;
       } else if ((mpt & 1) == 1) {                      // odd point: save (:654-658)
-        int s = 0;
-        while (s < a.d_max && table[s] != -1) ++s;      // find_next (a free slot always exists)
-        table[s] = mpt;
+        const int s = save_slot(mpt, a.d_max);
         vstore<M>(W, V_SLOTS, 2 * s, q);
         vstore<M>(W, V_SLOTS + 1, 2 * s, p);
       }
@@ -402,10 +429,7 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
     // even point: sub-tree U-turn checks against check_points(mpt) (:699-736), converged loop
     const bool checking = later && !reject && (mpt & 1) == 0;
     const int ncheck = checking ? cp_count(mpt) : 0;
-    int ncheck_w = ncheck;
-#pragma unroll
-    for (int off = 1; off < kWave; off <<= 1) ncheck_w = max(ncheck_w, __shfl_xor(ncheck_w, off, kWave));
-    ncheck_w = uniform_i(ncheck_w);
+    const int ncheck_w = wave_max_i32(ncheck);
     bool alive_chk = checking;
     // check points of mpt, incrementally (cp_point): mpt - r + 1, then + r/2, + r/4, ...
     int cp_half = checking ? cp_r(mpt) : 2;
@@ -416,10 +440,8 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
         cp_half >>= 1;
         cp_pt += cp_half;
       }
-      const int l = doit ? cp_pt : 0;
-      int s = 0;
-      if (doit)
-        while (s < a.d_max && table[s] != l) ++s;       // retrieve_save_index (unique match)
+      const int l = doit ? cp_pt : 1;
+      const int s = save_slot(l, a.d_max);              // retrieve_save_index (:715)
       double r_dot = 0.0, l_dot = 0.0;
       if (doit) {
         double qcv[M], pcv[M];
@@ -445,9 +467,7 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
         if (l_dot < 0.0 && r_dot < 0.0) {               // :727-732
           reject = true;
           alive_chk = false;
-        } else if (l > 1 && release_fast(mpt, l)) {     // :735-736
-          table[s] = -1;
-        }
+        }                                               // (release, :735-736: nothing to free)
       }
     }
     if (later && !reject) {                             // progressive sampling (:743-751)
@@ -457,8 +477,8 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
       pi_new = num + exp(E_max_now - E_max_prev) * pi_new;
       const double r = num / pi_new;
       if (draw(false) < r) {
-        vstore<M>(W, V_NEW_Q, 0, q);
-        gstore<MT>(W, V_NEW_G, 0, acc);
+        vstore<M>(W, V_OLD_Q, 2 - old2, q);
+        gstore<MT>(W, V_OLD_G, 2 - old2, acc);
         maha_new = maha_pt;
       }
       ++k;
@@ -478,12 +498,8 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
       E_max_old = fmax(E_max_old_prev, E_max_now);
       pi_old = exp(-(E_max_now - E_max_old)) * pi_new + exp(-(E_max_old_prev - E_max_old)) * pi_old;
       const double A = fmin(1.0, r);
-      if (draw(false) < A) {                            // :773-775
-        double t[M];
-        vload<M>(W, V_NEW_Q, 0, t);
-        vstore<M>(W, V_OLD_Q, 0, t);
-        vload<M>(W, V_NEW_G, 0, t);
-        vstore<M>(W, V_OLD_G, 0, t);
+      if (draw(false) < A) {                            // :773-775: old <- new, as a buffer swap
+        old2 = 2 - old2;
         maha_old = maha_new;
       }
       const int o = udir == 0 ? V_LEFT_Q : V_RIGHT_Q;   // the other end
@@ -513,8 +529,16 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
       } else if (d > a.d_max - 1) {                     // :596-598 (the reference aborts the run)
         ++n_dmax;
         state = S_ITER_END;
-      } else {
-        state = S_SUB_START;
+      } else {                                          // next doubling: its direction (:608) now
+        Lsub = 1 << d;
+        const int nd = (int)draw(true);
+        if (nd == udir) {                               // same end: it is (q, p, acc) in registers
+          k = 0;
+          state = S_READY;
+        } else {
+          udir = nd;
+          state = S_SUB_LOAD;
+        }
       }
     }
   }
@@ -540,19 +564,19 @@ __global__ __launch_bounds__(256, 1) void k_nuts_iters(RandArgs a) {
 template <int MT, bool EXACT>
 hipError_t launch_nuts_mt2(const RandArgs& a, bool gen, bool replay, hipStream_t s) {
   // persistent: one block per CU (LDS: P + index tables), chains handed out by the queue
-  const int64_t blocks = (a.n + 16 * kDenseWaves - 1) / (16 * kDenseWaves);
+  const int64_t blocks = (a.n + 16 * kNutsWaves - 1) / (16 * kNutsWaves);
   const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)device_cus())));
   const int64_t n_waves = (a.n + 15) / 16;
   const int64_t wave_doubles = (int64_t)(V_SLOTS + 2 * (a.d_max + 1)) * 4 * MT * kWave;
   double* queue = a.ws + n_waves * wave_doubles + n_waves * 16;
   if (hipError_t e = hipMemsetAsync(queue, 0, sizeof(unsigned long long), s)) return e;
-  const size_t lds = (size_t)MT * 4 * MT * kWave * sizeof(double) + kDenseWaves * 16 * kMaxDepth * sizeof(int);
+  const size_t lds = (size_t)MT * 4 * MT * kWave * sizeof(double);
   if (gen) {
-    if (replay) k_nuts_iters<MT, EXACT, true, true><<<grid, 64 * kDenseWaves, lds, s>>>(a);
-    else k_nuts_iters<MT, EXACT, true, false><<<grid, 64 * kDenseWaves, lds, s>>>(a);
+    if (replay) k_nuts_iters<MT, EXACT, true, true><<<grid, 64 * kNutsWaves, lds, s>>>(a);
+    else k_nuts_iters<MT, EXACT, true, false><<<grid, 64 * kNutsWaves, lds, s>>>(a);
   } else {
-    if (replay) k_nuts_iters<MT, EXACT, false, true><<<grid, 64 * kDenseWaves, lds, s>>>(a);
-    else k_nuts_iters<MT, EXACT, false, false><<<grid, 64 * kDenseWaves, lds, s>>>(a);
+    if (replay) k_nuts_iters<MT, EXACT, false, true><<<grid, 64 * kNutsWaves, lds, s>>>(a);
+    else k_nuts_iters<MT, EXACT, false, false><<<grid, 64 * kNutsWaves, lds, s>>>(a);
   }
   return hipGetLastError();
 }
