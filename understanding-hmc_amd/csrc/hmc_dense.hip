@@ -21,6 +21,13 @@
 #include "hmc_internal.hpp"
 #include "hmc_dense_ops.hpp"
 
+// Waves per block (one block per CU: the LDS copy of P).  8 = two waves per SIMD at 256 registers:
+// the kernel spills ~88 B per lane, but one wave's MFMA gradient overlaps the other's RNG,
+// kick/drift and load latency: +9.5% over one wave per SIMD (MFMA busy was 68%).
+#ifndef HMC_DENSE_WAVES
+#define HMC_DENSE_WAVES 8
+#endif
+
 namespace hmc {
 
 namespace {
@@ -419,9 +426,7 @@ void launch_dense_w(const DenseArgs& a, bool gen, bool replay, hipStream_t s) {
 
 template <int MT, bool EXACT>
 hipError_t launch_dense_mt2(const DenseArgs& a, bool gen, bool replay, hipStream_t s) {
-  // 4 waves (one per SIMD, all 512 registers): two waves per SIMD at 256 registers spill the
-  // leapfrog loop (q, p, gradient tile and P fragments need ~200 of them before addresses)
-  launch_dense_w<MT, EXACT, 4>(a, gen, replay, s);
+  launch_dense_w<MT, EXACT, HMC_DENSE_WAVES>(a, gen, replay, s);
   return hipGetLastError();
 }
 

@@ -77,6 +77,10 @@ __device__ __forceinline__ void gradient(const DenseArgs& a, const double* __res
 #pragma unroll
       for (int nt = 0; nt < MT; ++nt) an[nt] = frag(nt * KS + ks + 1);
     }
+    // keep the next k-step's fragment reads ahead of this k-step's MFMAs: scheduled after them
+    // (the compiler's choice without this barrier) the reads issued only once the 7 MFMAs had
+    // queued and the next k-step waited on their LDS latency
+    __builtin_amdgcn_sched_barrier(0);
     // padded dims (d >= D) meet zero columns of P, so no guard is needed here
     const double x = (GEN && a.q0) ? q[ks] - a.q0[min(h + 4 * ks, a.D - 1)] : q[ks];
 #pragma unroll
