@@ -141,8 +141,11 @@ typedef struct hmc_state {
   int64_t qc_row0;
   /* Dense targets, Random sampler: scratch of hmc_random_workspace_size() bytes for L-ordered
    * tiles (each iteration, chains are counting-sorted by trajectory length so that the 16
-   * chains sharing an MFMA tile integrate the same number of steps; results are unchanged).
-   * NULL = tiles in chain order (several iterations fused per launch).  Ignored for DIAG. */
+   * chains sharing an MFMA tile integrate the same number of steps; results are unchanged) and
+   * a per-chain cache of the gradient at q (reused instead of recomputed at the start of each
+   * iteration; bit-identical).  hmc_chain_init invalidates the cache: a caller that writes q
+   * itself must call hmc_chain_init again.  NULL = tiles in chain order (several iterations
+   * fused per launch), no cache.  Ignored for DIAG. */
   int32_t* order;
 } hmc_state;
 
@@ -163,7 +166,7 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
                             const hmc_replay* r /* NULL for Philox */, hmc_state* st, void* stream);
 
 /* Bytes of the optional hmc_state.order scratch for hmc_random_iters on this target
- * (0 for diagonal targets, which need none). */
+ * (0 for diagonal targets, which need none): the tile order plus the gradient cache. */
 int64_t hmc_random_workspace_size(const hmc_target* t, int64_t n_chains);
 /* Bytes of device workspace hmc_nuts_iters needs for n_chains chains (tree vectors: live
  * points, both boundaries, d_max+1 save slots; replay-tape cursors).  0 if unsupported. */

@@ -74,10 +74,12 @@ def test_no_cpu_fallback_when_library_missing(tmp_path, monkeypatch):
 
 def test_random_workspace_size_query(monkeypatch):
     """hmc_random_workspace_size: no scratch for diagonal targets; dense targets take an int32
-    chain order + two 256-bin histograms (host-only query, no GPU call)."""
+    chain order + two 256-bin histograms and the per-chain gradient cache (host-only query)."""
     from hmc_amd import _lib as H
     monkeypatch.setattr(H, "_lib", None)     # argtypes bound to this module's structure classes
     L = H.lib()
     assert L.hmc_random_workspace_size(ctypes.byref(H.Target(100, H.HMC_TARGET_DIAG, None, None, 0.0)), 1000) == 0
-    assert L.hmc_random_workspace_size(ctypes.byref(H.Target(100, H.HMC_TARGET_DENSE, None, None, 0.0)), 1000) == (1000 + 512) * 4
+    # int32 tile order + histograms, 16-byte aligned, a 16-byte validity word, the [n][D] gradient cache
+    assert L.hmc_random_workspace_size(ctypes.byref(H.Target(100, H.HMC_TARGET_DENSE, None, None, 0.0)), 1000) == \
+        (1000 + 512) * 4 + 16 + 1000 * 100 * 8
     assert L.hmc_random_workspace_size(None, 1000) == 0

@@ -403,3 +403,39 @@ def test_dense_mass_matrix_rows_and_stationarity():
     assert abs(np.corrcoef(last[:, 0], last[:, 1])[0, 1] - rho) < 6 * (1 - rho ** 2) / np.sqrt(N)
     assert 0.05 < a.accept_R < 1.0
     assert np.array_equal(a.q_chain, run().q_chain)
+
+
+def test_dense_checkpoint_resume_bitexact(tmp_path):
+    """Dense L-ordered engine (gradient cache in the workspace): checkpoint after iteration 3,
+    resume in a fresh engine, identical to the uninterrupted run; re-initialising q invalidates
+    the cache (the next launch recomputes every gradient)."""
+    from hmc_amd.engine import RandomEngine
+    from hmc_amd.target import MVNTarget
+    D, N, Niter = 100, 777, 7
+    cov = O.mvn_cov(D, 0.9)
+    q0 = np.random.RandomState(5).standard_normal((N, D)) @ np.linalg.cholesky(cov).T
+
+    def make():
+        e = RandomEngine(MVNTarget(np.zeros(D), cov), N, Niter, 1, 1, 5, 20, 0.1, rng="philox", seed=21,
+                         fp_mode="fast")
+        e.init(q0)
+        return e
+    ref = make()
+    for a in range(1, Niter + 1):
+        ref.run(a, a + 1)
+    a_ = make()
+    for a in range(1, 4):
+        a_.run(a, a + 1)
+    path = str(tmp_path / "dense.npz")
+    a_.save(path, 4)
+    b = RandomEngine(MVNTarget(np.zeros(D), cov), N, Niter, 1, 1, 5, 20, 0.1, rng="philox", seed=21, fp_mode="fast")
+    assert b.restore(path) == 4
+    for a in range(4, Niter + 1):
+        b.run(a, a + 1)
+    torch.cuda.synchronize()
+    assert torch.equal(b.q, ref.q) and torch.equal(b.q_chain, ref.q_chain) and torch.equal(b.E_chain, ref.E_chain)
+    a_.init(q0)                                   # same start again: same chains as ref's first iterations
+    for a in range(1, Niter + 1):
+        a_.run(a, a + 1)
+    torch.cuda.synchronize()
+    assert torch.equal(a_.q_chain, ref.q_chain)

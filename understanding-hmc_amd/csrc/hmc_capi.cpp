@@ -188,6 +188,12 @@ hmc_status hmc_chain_init(const hmc_target* t, const hmc_kinetic* k, const hmc_s
     const hmc::Layout lay{0, 0, 0, (t->D + 1) / 2};
     hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
     a.qstart = q_start;
+    if (st->order) {   // the gradient cache no longer matches q: the next launch recomputes it
+      int32_t* valid = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(st->order) +
+                                                  hmc::dense_gcache_offset_bytes(s->n_chains) - 16);
+      if (hmc_status e = hip_status(hipMemsetAsync(valid, 0, sizeof(int32_t), (hipStream_t)stream), "hmc_chain_init"))
+        return e;
+    }
     return hip_status(hmc::launch_dense_init(a, replay, (hipStream_t)stream), "hmc_chain_init(dense)");
   }
   const int L_lo = s->L_high > s->L_low ? s->L_low : 5, L_hi = s->L_high > s->L_low ? s->L_high : 20;
@@ -219,8 +225,23 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
     const hmc::Layout lay{0, 0, 0, (t->D + 1) / 2};
     hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
     const bool exact = s->fp_mode == HMC_MODE_EXACT;
-    if (!st->order || a.traj_q || !hmc::dense_order_ok(a))
-      return hip_status(hmc::launch_dense_iters(a, exact, replay, (hipStream_t)stream), "hmc_random_iters(dense)");
+    int32_t* gvalid = nullptr;
+    if (st->order) {   // gradient cache in the workspace (hmc_random_workspace_size)
+      char* base = reinterpret_cast<char*>(st->order);
+      gvalid = reinterpret_cast<int32_t*>(base + hmc::dense_gcache_offset_bytes(s->n_chains) - 16);
+      a.gcache = reinterpret_cast<double*>(base + hmc::dense_gcache_offset_bytes(s->n_chains));
+      a.gvalid = gvalid;
+    }
+    // every launch leaves the cache holding the gradient at each chain's q
+    auto mark_valid = [&]() -> hmc_status {
+      return gvalid ? hip_status(hipMemsetAsync(gvalid, 1, 1, (hipStream_t)stream), "hmc_random_iters") : HMC_OK;
+    };
+    if (!st->order || a.traj_q || !hmc::dense_order_ok(a)) {
+      if (hmc_status e = hip_status(hmc::launch_dense_iters(a, exact, replay, (hipStream_t)stream),
+                                    "hmc_random_iters(dense)"))
+        return e;
+      return mark_valid();
+    }
     // L-ordered tiles: one launch per iteration, chains counting-sorted by that iteration's L
     for (int it = s->iter_begin; it < s->iter_end; ++it) {
       if (hmc_status e = hip_status(hmc::launch_dense_order(a, it, replay, st->order, (hipStream_t)stream),
@@ -232,6 +253,7 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
       if (hmc_status e = hip_status(hmc::launch_dense_iters(a, exact, replay, (hipStream_t)stream),
                                     "hmc_random_iters(dense)"))
         return e;
+      if (hmc_status e = mark_valid()) return e;
     }
     return HMC_OK;
   }
@@ -256,8 +278,8 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
 }
 
 int64_t hmc_random_workspace_size(const hmc_target* t, int64_t n_chains) {
-  if (!t || n_chains < 0 || t->kind != HMC_TARGET_DENSE) return 0;
-  return hmc::dense_order_ints(n_chains) * (int64_t)sizeof(int32_t);
+  if (!t || n_chains < 0 || t->kind != HMC_TARGET_DENSE || t->D < 1) return 0;
+  return hmc::dense_workspace_bytes(n_chains, t->D);
 }
 
 int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max) {

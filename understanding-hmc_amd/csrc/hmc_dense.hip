@@ -75,6 +75,15 @@ void k_dense_iters(DenseArgs a) {
   }
   double Eprev = live ? a.Eprev[c] : 0.0;
   double* const qcb = a.qc ? a.qc + c * (int64_t)a.Lq * a.D : nullptr;
+  // gradient cache (L-ordered launches, one iteration each): the gradient at q is read with q
+  // instead of recomputed (13 -> 12 gradients per 12 leapfrogs); it is the value the MFMA tile
+  // computed at that q, so results are bit-identical.  Other launches keep it up to date.
+  double* const gch = a.gcache ? a.gcache + c * a.D + h : nullptr;
+  const bool g_read = a.gcache && a.order && a.gvalid && uniform_i(*a.gvalid) != 0;
+  if (g_read) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) acc[m >> 2][m & 3] = (live && dim_ok(m)) ? gch[4 * m] : 0.0;
+  }
   // chain-0 trajectory capture (samplers.py:442-452): the wave holding global chain 0 (lane 0;
   // capture runs never use a.order)
   const bool cap_wave = a.traj_q && uniform_i((int)(__builtin_amdgcn_readfirstlane((int)(gc & 0xffffffff)) == 0 &&
@@ -113,7 +122,14 @@ void k_dense_iters(DenseArgs a) {
       }
     }
     // ---- gradient at q and E0 = V(q) + K(p)  (:434)
-    gradient<MT, GEN>(a, sP, lane, h, q, acc);
+    if (!g_read || it != a.it0) {
+      gradient<MT, GEN>(a, sP, lane, h, q, acc);
+      if (gch && live) {              // keep the cache valid for rejections (q stays, so does g)
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+          if (dim_ok(m)) gch[4 * m] = gval<MT>(acc, m);
+      }
+    }
     double maha = 0.0, kin = 0.0;
     // (x . P x, p . Minv p) of this lane's dims.  Diagonal/identity mass: P x is the gradient
     // tile.  Dense mass: the tile holds Minv P x (the kick), so P x and Minv p are two more
@@ -230,6 +246,11 @@ void k_dense_iters(DenseArgs a) {
         if (accept) qh[4 * m] = q[m];
         else q[m] = qh[4 * m];
       }
+    }
+    if (gch && live && accept) {      // the gradient at the new q (a rejection keeps the cached one)
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        if (dim_ok(m)) gch[4 * m] = gval<MT>(acc, m);
     }
     if (live && write_row && qcb && row >= a.q_row0) {
       double* rowp = qcb + (row % a.Lq) * a.D + h;
@@ -468,6 +489,8 @@ hipError_t launch_dense_init(const DenseArgs& a, bool replay, hipStream_t s) {
 }
 
 int64_t dense_order_ints(int64_t n) { return n + 2 * kOrderBins; }
+int64_t dense_gcache_offset_bytes(int64_t n) { return ((dense_order_ints(n) * 4 + 15) / 16) * 16 + 16; }
+int64_t dense_workspace_bytes(int64_t n, int D) { return dense_gcache_offset_bytes(n) + n * (int64_t)D * 8; }
 
 bool dense_order_ok(const DenseArgs& a) { return a.L_high - a.L_low <= kOrderBins && a.n < (1ll << 31); }
 

@@ -55,6 +55,8 @@ struct RandArgs {
   int dbgL;              // forced trajectory length (HMC_DEBUG_L env; -1 in normal runs)
   unsigned long long* stamps;  // diagnostic phase timers (HMC_DEBUG_STAMPS env; null in normal runs)
   const int32_t* order;  // dense: tile slot -> chain (L-ordered tiles) or null (slot = chain)
+  double* gcache;        // dense: per-chain gradient at q [n][D] (in the order workspace) or null
+  const int32_t* gvalid; // dense: nonzero once gcache holds the gradient of every chain's q
   int64_t ntiles;        // dense: 16-chain tiles
 };
 
@@ -74,6 +76,9 @@ hipError_t launch_wave_iters(const RandArgs& a, int K, bool exact, bool gen, boo
 hipError_t launch_dense_init(const DenseArgs& a, bool replay, hipStream_t s);
 hipError_t launch_dense_iters(const DenseArgs& a, bool exact, bool replay, hipStream_t s);
 int64_t dense_order_ints(int64_t n);   // int32 scratch of the L-ordering (order[n] + histograms)
+// gradient cache inside the order workspace: validity word, then [n][D] doubles
+int64_t dense_gcache_offset_bytes(int64_t n);
+int64_t dense_workspace_bytes(int64_t n, int D);
 bool dense_order_ok(const DenseArgs& a);
 hipError_t launch_dense_order(const DenseArgs& a, int it, bool replay, int32_t* ws, hipStream_t s);
 int device_cus();

@@ -205,6 +205,8 @@ class RandomEngine:
             arr["E_chain"], arr["dE_chain"] = self.E_chain, self.dE_chain
         if getattr(self, "ws", None) is not None:
             arr["ws"] = self.ws
+        if self._order is not None:
+            arr["order_ws"] = self._order                   # dense: tile order + gradient cache of q
         if diag is not None:
             arr.update(diag_shift=diag.shift, diag_s1=diag.s1, diag_s2=diag.s2, diag_vsum=diag.vsum)
             st = getattr(self, "_stream", None)
@@ -224,7 +226,7 @@ class RandomEngine:
                 raise AssertionError(f"checkpoint does not match this engine: {bad}")
             for k, t in (("q", self.q), ("E_prev", self.E_prev), ("counters", self.counters),
                          ("q_chain", self.q_chain), ("E_chain", self.E_chain), ("dE_chain", self.dE_chain),
-                         ("ws", getattr(self, "ws", None))):
+                         ("ws", getattr(self, "ws", None)), ("order_ws", self._order)):
                 if t is not None and k in z.files:
                     t.copy_(torch.as_tensor(z[k]).to(self.device))
             if diag is not None:
