@@ -253,6 +253,9 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
   int it_base = a.it0 - kWave, draw_L = 0;
   double draw_lnu = 0.0;
 
+#ifdef HMC_UNROLL2
+#pragma unroll 2
+#endif
   for (int it = a.it0; it < a.it1; ++it) {
     const bool post = it >= a.wu;
     const bool write_row = post && ((it == a.niter) || (phase == a.thin - 1));
@@ -342,7 +345,9 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     } else if (L > 0) {
       // FAST: consecutive half kicks merged into one full kick, in shifted coordinates
       // u = q - q0 (2 FMA per coordinate per step instead of 3; same integrator, other rounding)
-      double u[2 * K], dtc[2 * K], kh[2 * K], kfull[2 * K];
+      // (without q0 the shift is the identity: integrate q in place, no copies in and out)
+      double ubuf[GEN ? 2 * K : 1], dtc[2 * K], kh[2 * K], kfull[2 * K];
+      double (&u)[2 * K] = *reinterpret_cast<double(*)[2 * K]>(GEN ? ubuf : q);
 #pragma unroll
       for (int j = 0; j < K; ++j) {
 #pragma unroll
@@ -352,7 +357,7 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
           kh[e] = -(GEN ? cc.hd * (cc.minv * cc.prec) : cc.hd);
           kfull[e] = 2.0 * kh[e];
           dtc[e] = cc.dt;
-          u[e] = GEN ? q[e] - cc.q0 : q[e];
+          if constexpr (GEN) u[e] = q[e] - cc.q0;
           p[e] = __builtin_fma(kh[e], u[e], p[e]);          // first half kick
         }
       }
@@ -378,38 +383,46 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
         p[e] = __builtin_fma(kh[e], u[e], p[e]);            // last half kick
       }
       capture(L - 1);
+      if constexpr (GEN) {
 #pragma unroll
-      for (int j = 0; j < K; ++j) {
+        for (int j = 0; j < K; ++j) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int e = 2 * j + h;
-          q[e] = GEN ? u[e] + slot_const<GEN>(a, kk[j], h, pv[j]).q0 : u[e];
+          for (int h = 0; h < 2; ++h) {
+            const int e = 2 * j + h;
+            q[e] = u[e] + slot_const<GEN>(a, kk[j], h, pv[j]).q0;
+          }
         }
       }
     }
 
-    // next iteration's momentum (keyed by it+1) so its kinetic energy joins this reduction
-    const bool more = it + 1 < a.it1;
-    double kn = 0.0;
-    if (more && !(FULL && (a.dbg & 256))) {
-      if constexpr (RING) ring_momentum(it + 1, pn);
-      else wave_momentum<K, GEN, REPLAY>(a, c, gc, it + 1, kk, pv, pn, s_ntab);
-      if constexpr (FASTID) {
-        kn = pn[1] * pn[1];
-        kn = __builtin_fma(pn[0], pn[0], kn);
-#pragma unroll
-        for (int e = 2; e < 2 * K; ++e) kn = __builtin_fma(pn[e], pn[e], kn);
-      } else {
-        kn = kin_partial<K, GEN>(a, kk, pv, pn);
-      }
-    }
-    double m1, k1, m1l;
-    bool accept;
+    // FASTID: E1's partials and DPP chain first; p is then dead, so the next momentum is drawn
+    // into p itself (no copy at the end of the iteration)
+    double m1 = 0.0, k1 = 0.0, m1l = 0.0, s1 = 0.0;
     if constexpr (FASTID) {
       wave_partials_fma<K>(q, p, m1l, k1);
       m1 = m1l;
+      s1 = wave_sum_dpp_l63(k1);
+    }
+    // next iteration's momentum (keyed by it+1) so its kinetic energy joins this reduction
+    const bool more = it + 1 < a.it1;
+    double kn = 0.0;
+    double (&pnext)[2 * K] = FASTID ? p : pn;
+    if (more && !(FULL && (a.dbg & 256))) {
+      if constexpr (RING) ring_momentum(it + 1, pnext);
+      else wave_momentum<K, GEN, REPLAY>(a, c, gc, it + 1, kk, pv, pnext, s_ntab);
+      if constexpr (FASTID) {
+        kn = pnext[1] * pnext[1];
+        kn = __builtin_fma(pnext[0], pnext[0], kn);
+#pragma unroll
+        for (int e = 2; e < 2 * K; ++e) kn = __builtin_fma(pnext[e], pnext[e], kn);
+      } else {
+        kn = kin_partial<K, GEN>(a, kk, pv, pnext);
+      }
+    }
+    bool accept;
+    if constexpr (FASTID) {
       // E1 - E0 and the test in lane 63, where the DPP chain leaves the total (samplers.py:459-462)
-      const double dE = __builtin_fma(wave_sum_dpp_l63(k1), 0.5, hlogc) - E0;
+      const double dE = __builtin_fma(s1, 0.5, hlogc) - E0;
 #ifdef HMC_AB_SELECT
       accept = __builtin_amdgcn_ballot_w64((dE < 0.0) || (lnu < -dE)) >> 63;
 #else
@@ -456,8 +469,10 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     n_lf2 += Lp * Lp;
     // advance
     if (more) {
+      if constexpr (!FASTID) {
 #pragma unroll
-      for (int e = 0; e < 2 * K; ++e) p[e] = pn[e];
+        for (int e = 0; e < 2 * K; ++e) p[e] = pn[e];
+      }
       if constexpr (EXACT) {
         m0 = accept ? m1 : m0;
         E0 = 0.5 * (a.logc + (m0 + kn));
