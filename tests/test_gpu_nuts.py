@@ -121,3 +121,38 @@ def test_nuts_philox_statistics(D, rho):
     assert h.n_leapfrog > N * 6 * 3
     h2 = run()
     assert np.array_equal(h.q_chain, h2.q_chain)
+
+
+@pytest.mark.parametrize("fp_mode", ["exact", "fast"])
+def test_nuts_full_cov_p_matches_oracle(fp_mode):
+    """NUTS with a full (non-diagonal) cov_p (Q3: p ~ N(0, cov_p), K = p.inv(cov_p).p/2, kick by
+    inv(cov_p).dVdq; samplers.py:352-356, :811-839 through gen_sample_NUTS :495-808), replayed
+    draws vs the oracle; plus Philox determinism."""
+    from hmc_amd.target import MVNTarget
+    import make_golden_shapes as S
+    D, N, Niter, wu, dt, d_max = 12, 5, 10, 2, 0.15, 9
+    rs = np.random.RandomState(77)
+    cov, cov_p = O.mvn_cov(D, 0.6), S.dense_cov_p(D)
+    C = np.linalg.cholesky(cov_p)
+    q_start = rs.standard_normal((N, D)) * 1.5
+    p0 = rs.standard_normal((N, D)) @ C.T
+    P = rs.standard_normal((N, Niter, D)) @ C.T
+    tape = rs.uniform(0.0, 2.0, (N, Niter * 2 * (2 ** d_max + d_max + 2)))
+    core = O.HMCCore(O.MVNTarget(np.zeros(D), cov), dt, cov_p)
+    ref = O.gen_sample_nuts(core, q_start, N, Niter, wu, 1, d_max, O.ReplayDraws(p0, P, tape=tape.copy()),
+                            on_dmax="break")
+    h = _nuts(D, MVNTarget(np.zeros(D), cov), N, Niter, wu, 1, dt, d_max, cov_p=cov_p, rng="replay",
+              fp_mode=fp_mode)
+    h.set_nuts_replay(p0, P, tape)
+    h.gen_sample_NUTS(q_start, 0, False, on_dmax="break")
+    assert h.n_leapfrog == ref["n_leapfrog"]
+    assert h.N_total_steps == ref["N_total_steps"]
+    np.testing.assert_allclose(h.q_chain, ref["q_chain"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(h.E_chain[:, :, 0], ref["E_chain"], rtol=1e-10, atol=1e-10)
+    runs = []
+    for _ in range(2):
+        g = _nuts(D, MVNTarget(np.zeros(D), cov), 64, 6, 1, 1, dt, d_max, cov_p=cov_p, rng="philox", seed=3,
+                  fp_mode=fp_mode)
+        g.gen_sample_NUTS(q_start[np.arange(64) % N], 0, False, on_dmax="break")
+        runs.append(g.q_chain)
+    assert np.array_equal(runs[0], runs[1]) and np.isfinite(runs[0]).all()

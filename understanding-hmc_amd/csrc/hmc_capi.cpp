@@ -297,8 +297,7 @@ hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_s
   if (s->n_chains == 0) return HMC_OK;   // empty batch: zero-size buffers may be NULL
   if (!st->q || !st->E_prev) return fail(HMC_EINVAL, "null state");
   if (s->d_max < 1 || s->d_max > 15) return fail(HMC_EINVAL, "d_max must be in [1, 15]");
-  if (k->minv_full || k->p_chol_t || k->kick)
-    return fail(HMC_ENOTSUP, "NUTS: dense (non-diagonal) mass matrix not supported");
+  if (hmc_status e = check_mass(t, k, s)) return e;
   if (t->kind != HMC_TARGET_DENSE) return fail(HMC_ENOTSUP, "NUTS runs the dense kernel: pass prec as dense");
   if (!hmc::dense_tiles(t->D)) return fail(HMC_ENOTSUP, "dense target: D=%d > 128 not supported", t->D);
   const bool replay = s->rng_mode == HMC_RNG_REPLAY;

@@ -169,7 +169,10 @@ __device__ __forceinline__ double mac(double acc, double x, double y) {
   else return __builtin_fma(x, y, acc);
 }
 
-template <int MT, bool EXACT, bool GEN, bool REPLAY>
+// MASS: full (non-diagonal) cov_p (implies GEN): LDS holds the kick matrix inv(cov_p).P
+// (stage_precision), p = C z, and every energy takes P x and inv(cov_p) p from two L2 products
+// (matvec_global) in converged code.  Its own instantiation, like the dense Random kernel's.
+template <int MT, bool EXACT, bool GEN, bool REPLAY, bool MASS = false>
 __global__ __launch_bounds__(64 * kNutsWaves) __attribute__((amdgpu_waves_per_eu(kNutsWaves / 4, kNutsWaves / 4)))
 void k_nuts_iters(RandArgs a) {
   constexpr int M = 4 * MT;
@@ -285,10 +288,11 @@ void k_nuts_iters(RandArgs a) {
 #pragma unroll
           for (int m = 0; m < M; ++m) {
             const double z = (h + 4 * m < a.D) ? row[h + 4 * m] : 0.0;
+            p[m] = z;
+            if constexpr (MASS) continue;               // K and the boundaries after the products below
             kin += z * (dim_minv<MT, GEN>(a, h + 4 * m) * z);
             vput<M>(W, V_RIGHT_P, m, z);
             vput<M>(W, V_LEFT_P, m, -z);
-            p[m] = z;
           }
         } else {
 #pragma unroll
@@ -302,13 +306,42 @@ void k_nuts_iters(RandArgs a) {
             }
             z0 = d0 < a.D ? z0 : 0.0;
             z1 = d1 < a.D ? z1 : 0.0;
-            kin += z0 * (dim_minv<MT, GEN>(a, d0) * z0);
-            kin += z1 * (dim_minv<MT, GEN>(a, d1) * z1);
-            vput2<M>(W, V_RIGHT_P, m, z0, z1);
-            vput2<M>(W, V_LEFT_P, m, -z0, -z1);
             p[m] = z0;
             p[m + 1] = z1;
+            if constexpr (!MASS) {
+              kin += z0 * (dim_minv<MT, GEN>(a, d0) * z0);
+              kin += z1 * (dim_minv<MT, GEN>(a, d1) * z1);
+              vput2<M>(W, V_RIGHT_P, m, z0, z1);
+              vput2<M>(W, V_LEFT_P, m, -z0, -z1);
+            }
             __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+      if constexpr (MASS) {                             // converged: the products need every lane
+        if (__builtin_amdgcn_ballot_w64(starting)) {
+          d4 t[MT];
+          double pc[M];
+          if constexpr (!REPLAY) {                      // p = C z ~ N(0, cov_p) (samplers.py:829)
+            matvec_global<MT>(a.cholt, a.D, lane, p, t);
+#pragma unroll
+            for (int m = 0; m < M; ++m) pc[m] = (h + 4 * m < a.D) ? gval<MT>(t, m) : 0.0;
+          } else {
+#pragma unroll
+            for (int m = 0; m < M; ++m) pc[m] = p[m];
+          }
+          matvec_global<MT>(a.minvf, a.D, lane, pc, t);
+          double kk = 0.0;
+#pragma unroll
+          for (int m = 0; m < M; ++m) kk = mac<EXACT>(kk, pc[m], gval<MT>(t, m));
+          if (starting) {
+            kin = kk;
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+              p[m] = pc[m];
+              vput<M>(W, V_RIGHT_P, m, pc[m]);
+              vput<M>(W, V_LEFT_P, m, -pc[m]);
+            }
           }
         }
       }
@@ -385,13 +418,26 @@ void k_nuts_iters(RandArgs a) {
       }
     }
     double mp1 = 0.0, kp1 = 0.0;
+    if constexpr (MASS) {                               // x.P.x and p.inv(cov_p).p (acc holds the kick)
+      double xv[M];
+      d4 t[MT];
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const int dd = h + 4 * m;
-      const double mi = dim_minv<MT, GEN>(a, dd);
-      mp1 = mac<EXACT>(mp1, (GEN && a.q0) ? q[m] - a.q0[min(dd, a.D - 1)] : q[m], gval<MT>(acc, m));
-      kp1 = mac<EXACT>(kp1, p[m], mi * p[m]);
-      if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      for (int m = 0; m < M; ++m) xv[m] = a.q0 ? q[m] - a.q0[min(h + 4 * m, a.D - 1)] : q[m];
+      matvec_global<MT>(a.prec, a.D, lane, xv, t);
+#pragma unroll
+      for (int m = 0; m < M; ++m) mp1 = mac<EXACT>(mp1, xv[m], gval<MT>(t, m));
+      matvec_global<MT>(a.minvf, a.D, lane, p, t);
+#pragma unroll
+      for (int m = 0; m < M; ++m) kp1 = mac<EXACT>(kp1, p[m], gval<MT>(t, m));
+    } else {
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const int dd = h + 4 * m;
+        const double mi = dim_minv<MT, GEN>(a, dd);
+        mp1 = mac<EXACT>(mp1, (GEN && a.q0) ? q[m] - a.q0[min(dd, a.D - 1)] : q[m], gval<MT>(acc, m));
+        kp1 = mac<EXACT>(kp1, p[m], mi * p[m]);
+        if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      }
     }
     const double maha_pt = chain_sum4(mp1);
     const double E_tmp = 0.5 * (a.logc + (maha_pt + chain_sum4(kp1)));   // E (:618 / :643)
@@ -571,7 +617,10 @@ hipError_t launch_nuts_mt2(const RandArgs& a, bool gen, bool replay, hipStream_t
   double* queue = a.ws + n_waves * wave_doubles + n_waves * 16;
   if (hipError_t e = hipMemsetAsync(queue, 0, sizeof(unsigned long long), s)) return e;
   const size_t lds = (size_t)MT * 4 * MT * kWave * sizeof(double);
-  if (gen) {
+  if (a.minvf) {
+    if (replay) k_nuts_iters<MT, EXACT, true, true, true><<<grid, 64 * kNutsWaves, lds, s>>>(a);
+    else k_nuts_iters<MT, EXACT, true, false, true><<<grid, 64 * kNutsWaves, lds, s>>>(a);
+  } else if (gen) {
     if (replay) k_nuts_iters<MT, EXACT, true, true><<<grid, 64 * kNutsWaves, lds, s>>>(a);
     else k_nuts_iters<MT, EXACT, true, false><<<grid, 64 * kNutsWaves, lds, s>>>(a);
   } else {
@@ -595,7 +644,7 @@ int64_t nuts_ws_doubles(int64_t n, int D, int d_max) {
 }
 
 hipError_t launch_nuts_iters(const RandArgs& a, bool exact, bool replay, hipStream_t s) {
-  const bool gen = a.q0 || a.minv || a.pscale || a.dtv;
+  const bool gen = a.q0 || a.minv || a.pscale || a.dtv || a.minvf;
   switch (dense_tiles(a.D)) {
     case 1: return launch_nuts_mt<1>(a, exact, gen, replay, s);
     case 2: return launch_nuts_mt<2>(a, exact, gen, replay, s);

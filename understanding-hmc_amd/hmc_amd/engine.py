@@ -255,8 +255,6 @@ class NutsEngine(RandomEngine):
                          fp_mode=fp_mode, chain_offset=chain_offset, store_chain=store_chain,
                          store_energy=store_energy, n_save=0, device=device, dense=True)
         assert on_dmax in ("raise", "break")
-        if self._minv_full is not None:
-            raise NotImplementedError("NUTS kernel: non-diagonal cov_p is not supported (Random sampler only)")
         self.d_max = int(d_max)
         self.on_dmax = 0 if on_dmax == "raise" else 1
         nbytes = H.lib().hmc_nuts_workspace_size(self.D, self.N, self.d_max)
