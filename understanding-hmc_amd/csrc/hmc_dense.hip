@@ -34,6 +34,13 @@ namespace {
 
 // WAVES waves per block, one block per CU (the LDS copy of P); WAVES = 4: one wave per SIMD
 // with the whole 512-register file.
+#ifndef HMC_DENSE_DB
+#define HMC_DENSE_DB 0
+#endif
+// fragment double buffering only with one wave per SIMD (HMC_DENSE_DB=1 forces it: A/B)
+template <int WAVES>
+constexpr bool kDenseDB = WAVES <= 4 || HMC_DENSE_DB;
+
 // MASS: dense (non-diagonal) mass matrix (implies GEN): its own instantiation, so the extra
 // products' registers never touch the diagonal-mass kernels.
 template <int MT, bool EXACT, bool GEN, bool REPLAY, int WAVES, bool MASS = false>
@@ -123,7 +130,7 @@ void k_dense_iters(DenseArgs a) {
     }
     // ---- gradient at q and E0 = V(q) + K(p)  (:434)
     if (!g_read || it != a.it0) {
-      gradient<MT, GEN>(a, sP, lane, h, q, acc);
+      gradient<MT, GEN, kDenseDB<WAVES>>(a, sP, lane, h, q, acc);
       if (gch && live) {              // keep the cache valid for rejections (q stays, so does g)
 #pragma unroll
         for (int m = 0; m < M; ++m)
@@ -213,7 +220,7 @@ void k_dense_iters(DenseArgs a) {
           if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
       }
-      gradient<MT, GEN>(a, sP, lane, h, q, acc);
+      gradient<MT, GEN, kDenseDB<WAVES>>(a, sP, lane, h, q, acc);
       if (act) {
 #pragma unroll
         for (int m = 0; m < M; ++m) {

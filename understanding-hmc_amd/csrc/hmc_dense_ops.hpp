@@ -50,7 +50,10 @@ struct FragReader {
   __device__ __forceinline__ double operator()(int f) const { return f < 128 ? lo[f * kWave] : hi[(f - 128) * kWave]; }
 };
 
-template <int MT, bool GEN>
+// DB: fragments of the next k-step read while this one's MFMAs run (one wave per SIMD must hide
+// the LDS latency itself); without it the reads sit right before their MFMAs and a second wave
+// on the SIMD covers the latency, for MT fewer live registers.
+template <int MT, bool GEN, bool DB = true>
 __device__ __forceinline__ void gradient(const DenseArgs& a, const double* __restrict__ sP, int lane, int h,
                                          const double (&q)[4 * MT], d4 (&acc)[MT]) {
   // k-step ks: MT MFMAs (one per 16-dim output tile) with the P fragments of ks, while the
@@ -64,6 +67,22 @@ __device__ __forceinline__ void gradient(const DenseArgs& a, const double* __res
   // they carry the (scalar) exit test.
   const int ks_end = __builtin_amdgcn_readfirstlane((a.D + 3) >> 2);
   const FragReader frag(sP, lane);
+  if constexpr (!DB) {
+#pragma unroll
+    for (int nt = 0; nt < MT; ++nt) acc[nt] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks >= KS - 3 && ks >= ks_end) break;
+      double af[MT];
+#pragma unroll
+      for (int nt = 0; nt < MT; ++nt) af[nt] = frag(nt * KS + ks);
+      const double x = (GEN && a.q0) ? q[ks] - a.q0[min(h + 4 * ks, a.D - 1)] : q[ks];
+#pragma unroll
+      for (int nt = 0; nt < MT; ++nt) acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[nt], x, acc[nt], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return;
+  }
   double af[MT], an[MT];
 #pragma unroll
   for (int nt = 0; nt < MT; ++nt) {
