@@ -79,7 +79,13 @@ def test_random_workspace_size_query(monkeypatch):
     monkeypatch.setattr(H, "_lib", None)     # argtypes bound to this module's structure classes
     L = H.lib()
     assert L.hmc_random_workspace_size(ctypes.byref(H.Target(100, H.HMC_TARGET_DIAG, None, None, 0.0)), 1000) == 0
+    assert L.hmc_random_workspace_size(ctypes.byref(H.Target(2048, H.HMC_TARGET_DIAG, None, None, 0.0)), 1000) == 0
     # int32 tile order + histograms, 16-byte aligned, a 16-byte validity word, the [n][D] gradient cache
     assert L.hmc_random_workspace_size(ctypes.byref(H.Target(100, H.HMC_TARGET_DENSE, None, None, 0.0)), 1000) == \
         (1000 + 512) * 4 + 16 + 1000 * 100 * 8
     assert L.hmc_random_workspace_size(None, 1000) == 0
+    # large D (hmc_big.hip): p, q copy (+ gradient and its copy for dense) [n][D] and three [n] arrays
+    assert L.hmc_random_workspace_size(ctypes.byref(H.Target(3000, H.HMC_TARGET_DIAG, None, None, 0.0)), 1000) == \
+        2 * 1000 * 3000 * 8 + 3 * 8192
+    assert L.hmc_random_workspace_size(ctypes.byref(H.Target(200, H.HMC_TARGET_DENSE, None, None, 0.0)), 1000) == \
+        4 * 1000 * 200 * 8 + 3 * 8192

@@ -183,8 +183,17 @@ hmc_status hmc_chain_init(const hmc_target* t, const hmc_kinetic* k, const hmc_s
   const bool replay = s->rng_mode == HMC_RNG_REPLAY;
   if (replay && (!r || !r->p0)) return fail(HMC_EINVAL, "replay mode needs p0");
   if (s->n_chains == 0) return HMC_OK;
+  const bool dense = t->kind == HMC_TARGET_DENSE;
+  if (hmc::big_path(dense, t->D)) {   // large D: chain state in the workspace (hmc_big.hip)
+    if (k->minv_full) return fail(HMC_ENOTSUP, "full cov_p with D=%d: not supported", t->D);
+    if (!st->order) return fail(HMC_EINVAL, "D=%d needs hmc_random_workspace_size() bytes in state.order", t->D);
+    const hmc::Layout lay{0, 0, 0, (t->D + 1) / 2};
+    hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
+    a.qstart = q_start;
+    return hip_status(hmc::launch_big_init(hmc::big_args(a, st->order, dense), dense, replay, (hipStream_t)stream),
+                      "hmc_chain_init(large D)");
+  }
   if (t->kind == HMC_TARGET_DENSE) {
-    if (!hmc::dense_tiles(t->D)) return fail(HMC_ENOTSUP, "dense target: D=%d > 128 not supported", t->D);
     const hmc::Layout lay{0, 0, 0, (t->D + 1) / 2};
     hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
     a.qstart = q_start;
@@ -220,8 +229,18 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
   if (s->n_chains == 0 || s->iter_end == s->iter_begin) return HMC_OK;
   if (st->n_save > 0 && st->traj_q && st->traj_stride < s->L_high)
     return fail(HMC_EINVAL, "traj_stride must be >= L_high");
+  const bool dense = t->kind == HMC_TARGET_DENSE;
+  if (hmc::big_path(dense, t->D)) {   // large D (hmc_big.hip)
+    if (k->minv_full) return fail(HMC_ENOTSUP, "full cov_p with D=%d: not supported", t->D);
+    if (st->n_save > 0 && st->traj_q) return fail(HMC_ENOTSUP, "trajectory capture with D=%d: not supported", t->D);
+    if (!st->order) return fail(HMC_EINVAL, "D=%d needs hmc_random_workspace_size() bytes in state.order", t->D);
+    const hmc::Layout lay{0, 0, 0, (t->D + 1) / 2};
+    hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
+    return hip_status(hmc::launch_big_iters(hmc::big_args(a, st->order, dense), dense,
+                                            s->fp_mode == HMC_MODE_EXACT, replay, (hipStream_t)stream),
+                      "hmc_random_iters(large D)");
+  }
   if (t->kind == HMC_TARGET_DENSE) {
-    if (!hmc::dense_tiles(t->D)) return fail(HMC_ENOTSUP, "dense target: D=%d > 128 not supported", t->D);
     const hmc::Layout lay{0, 0, 0, (t->D + 1) / 2};
     hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
     const bool exact = s->fp_mode == HMC_MODE_EXACT;
@@ -278,7 +297,10 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
 }
 
 int64_t hmc_random_workspace_size(const hmc_target* t, int64_t n_chains) {
-  if (!t || n_chains < 0 || t->kind != HMC_TARGET_DENSE || t->D < 1) return 0;
+  if (!t || n_chains < 0 || t->D < 1) return 0;
+  const bool dense = t->kind == HMC_TARGET_DENSE;
+  if (hmc::big_path(dense, t->D)) return hmc::big_workspace_bytes(n_chains, t->D, dense);
+  if (!dense) return 0;
   return hmc::dense_workspace_bytes(n_chains, t->D);
 }
 

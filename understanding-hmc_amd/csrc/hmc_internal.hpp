@@ -84,6 +84,24 @@ hipError_t launch_dense_order(const DenseArgs& a, int it, bool replay, int32_t* 
 int device_cus();
 
 
+// Large-D Random sampler (hmc_big.hip): dense D > 128, diagonal D > 2048; chain state in HBM,
+// one iteration = begin, per leapfrog step (kick + drift, gradient, kick), end.
+struct BigArgs {
+  RandArgs a;
+  double* p;     // [n][D] momentum
+  double* g;     // [n][D] gradient at q (dense targets)
+  double* qi;    // [n][D] q at the start of the iteration (restored on rejection)
+  double* gi;    // [n][D] its gradient (dense targets)
+  int32_t* L;    // [n] trajectory length of the current iteration
+  double* lnu;   // [n] log u of the current iteration
+  double* E0;    // [n] energy at the start of the current iteration
+};
+bool big_path(int kind_dense, int D);
+int64_t big_workspace_bytes(int64_t n, int D, bool dense);
+BigArgs big_args(const RandArgs& a, void* ws, bool dense);
+hipError_t launch_big_init(const BigArgs& b, bool dense, bool replay, hipStream_t s);
+hipError_t launch_big_iters(const BigArgs& b, bool dense, bool exact, bool replay, hipStream_t s);
+
 // Row-wise API kernels (hmc_api_kernels.hip).
 struct RowArgs {
   int64_t n;
