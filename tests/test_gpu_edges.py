@@ -71,12 +71,14 @@ def test_empty_chain_batch():
 
 
 def test_unsupported_shapes_raise():
-    """Diagonal D > 2048 and dense D > 128 are outside the kernels: NotImplementedError, no launch."""
-    from hmc_amd.engine import RandomEngine
+    """What the kernels still leave out raises NotImplementedError with no launch: NUTS above
+    D = 128, and a full cov_p above D = 128 (the large-D Random path takes a diagonal mass only)."""
+    from hmc_amd.engine import NUTSEngine, RandomEngine
     from hmc_amd.target import MVNTarget
-    eng = RandomEngine(MVNTarget(np.zeros(2049), np.eye(2049)), 2, 4, 0, 1, 5, 20, 0.1, rng="philox")
     with pytest.raises(NotImplementedError):
-        eng.init(np.zeros((2, 2049)))
-    eng = RandomEngine(MVNTarget(np.zeros(129), O.mvn_cov(129, 0.5)), 2, 4, 0, 1, 5, 20, 0.1, rng="philox")
+        NUTSEngine(MVNTarget(np.zeros(129), O.mvn_cov(129, 0.5)), 2, 4, 0, 1, 6, 0.1, rng="philox")
+    D = 136
+    eng = RandomEngine(MVNTarget(np.zeros(D), O.mvn_cov(D, 0.5)), 2, 4, 0, 1, 5, 20, 0.1, rng="philox",
+                       cov_p=O.mvn_cov(D, 0.3))
     with pytest.raises(NotImplementedError):
-        eng.init(np.zeros((2, 129)))
+        eng.init(np.zeros((2, D)))
