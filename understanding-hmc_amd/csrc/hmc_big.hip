@@ -152,7 +152,6 @@ __global__ __launch_bounds__(256) void k_big_grad(BigArgs b, int l) {
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) acc[nt] = d4{0.0, 0.0, 0.0, 0.0};
   const int ks_end = (D + 3) >> 2;
-#pragma unroll 2
   for (int ks = 0; ks < ks_end; ++ks) {
     const int k = 4 * ks + h;
     const int kc = k < D ? k : D - 1;

@@ -386,8 +386,32 @@ __device__ __forceinline__ double wave_sum_dpp_l63(double v) {
 __device__ __forceinline__ double wave_sum_dpp(double v) { return readlane_d(wave_sum_dpp_l63(v), 63); }
 
 // Lane 63's bit of a compare mask as a wave-uniform bool (EXEC must be all ones): the sign of the
-// mask's high word, tested on the SALU.
-__device__ __forceinline__ bool lane63(uint64_t mask) { return (int32_t)(uint32_t)(mask >> 32) < 0; }
+// mask's bit 63, tested on the SALU (written in C the compiler emits a VALU 64-bit compare of the
+// SGPR pair for it and for its negation).
+__device__ __forceinline__ bool lane63(uint64_t mask) {
+  int r;
+  asm("s_bitcmp1_b64 %1, 63\n\ts_cselect_b32 %0, 1, 0" : "=s"(r) : "s"(mask) : "scc");
+  return r != 0;
+}
+
+// Parks v (valid in lane 63, where a DPP reduction leaves its total) in lane n of buf: two
+// ds_bpermute reads broadcast lane 63 over the LDS crossbar and the lane mask 1 << n is formed on
+// the SALU, so the park costs two v_cndmask (VALU) instead of two v_readlane plus a compare and
+// two selects.  (gfx950 has no wave-wide DPP rotate: wave_ror assembles but moves nothing.)
+// bp63: the byte address of lane 63, (kWave - 1) * 4, made opaque once outside the loop (a
+// literal lets the compiler turn the permute back into v_readlane + v_mov).
+__device__ __forceinline__ double park_lane(double buf, double v, int n, int bp63) {
+  const int src = bp63;
+  const uint32_t vlo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)__double2loint(v));
+  const uint32_t vhi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)__double2hiint(v));
+  uint64_t m;
+  asm("s_lshl_b64 %0, 1, %1" : "=s"(m) : "s"(n) : "scc");
+  uint32_t lo = __double2loint(buf), hi = __double2hiint(buf);
+  asm("v_cndmask_b32_e64 %0, %0, %2, %4\n\tv_cndmask_b32_e64 %1, %1, %3, %4"
+      : "+v"(lo), "+v"(hi)
+      : "v"(vlo), "v"(vhi), "s"(m));
+  return __hiloint2double(hi, lo);
+}
 
 __device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
 

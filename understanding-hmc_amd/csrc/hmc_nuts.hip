@@ -25,7 +25,6 @@ namespace hmc {
 
 namespace {
 
-constexpr int kMaxDepth = 16;   // table size bound (d_max <= 15)
 
 // Waves per block (one block per CU: the LDS copy of P), one per SIMD with the whole register file.
 // 8 (two waves per SIMD, 256 registers each) was measured at 0.42x: the step spills ~560 B per lane

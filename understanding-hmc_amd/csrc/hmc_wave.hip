@@ -95,7 +95,7 @@ __device__ __forceinline__ void wave_momentum(const RandArgs& a, int64_t c, uint
         const double* row = a.rp + (c * (int64_t)a.niter + (it - 1)) * a.D;
         load_pair(row, kk[j], even, d + 1 < a.D, p[2 * j], p[2 * j + 1]);
       } else {
-        normal_pair_tab(draw_block((uint32_t)kk[j], (uint32_t)it, gc, a.k0, a.k1), tab, p[2 * j], p[2 * j + 1]);
+        normal_pair_tab(draw_block_uc((uint32_t)kk[j], (uint32_t)it, gc, a.k0, a.k1), tab, p[2 * j], p[2 * j + 1]);
         if (GEN && a.pscale) {
           p[2 * j] *= a.pscale[d];
           if (d + 1 < a.D) p[2 * j + 1] *= a.pscale[d + 1];
@@ -160,7 +160,7 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     const int base = (it - a.it0) * a.npairs;
     if (gen_n < base + a.npairs) {                       // wave-uniform
       double z0, z1;
-      normal_pair_tab(draw_block((uint32_t)gk, (uint32_t)git, gc, a.k0, a.k1), s_ntab, z0, z1);
+      normal_pair_tab(draw_block_uc((uint32_t)gk, (uint32_t)git, gc, a.k0, a.k1), s_ntab, z0, z1);
       if constexpr (ODD) z1 = gk == a.npairs - 1 ? 0.0 : z1;   // dimension D does not exist
       *reinterpret_cast<double2*>(ring + 2 * ((gen_n + lane) & (kRingPairs - 1))) = make_double2(z0, z1);
       __builtin_amdgcn_wave_barrier();
@@ -220,7 +220,7 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     k0 = wave_sum_dpp(m0 + k0);
   }
   double E0 = EXACT ? 0.5 * (a.logc + (m0 + k0))
-                    : (FASTID ? __builtin_fma(wave_sum_dpp(k0), 0.5, hlogc) : 0.5 * (a.logc + k0));
+                    : (FASTID ? __builtin_fma(wave_sum_dpp_l63(k0), 0.5, hlogc) : 0.5 * (a.logc + k0));
 
   // thinning bookkeeping without divisions: row = (it - wu)//thin, phase = (it - wu) % thin
   int row = 0, phase = 0;
@@ -232,6 +232,7 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
   double Ebuf = 0.0, dEbuf = 0.0, Eprev_first = 0.0;
   int row_first = 0, nbuf = 0;
   const bool thin1 = a.thin == 1;
+  const int bp63 = (int)opaque_u32((kWave - 1) * 4);     // park_lane's source lane (byte address)
   double* const Ec = a.Ec ? a.Ec + c * (int64_t)a.Lc : nullptr;
   double* const dEc = a.dEc ? a.dEc + c * (int64_t)a.Lc : nullptr;
   double* const qcb = a.qc ? a.qc + c * (int64_t)a.Lq * a.D : nullptr;
@@ -239,7 +240,7 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     double dE = dEbuf;
     if (thin1) {
       const double before = __shfl_up(Ebuf, 1, kWave);
-      dE = Ebuf - (lane == 0 ? Eprev_first : before);
+      dE = Ebuf - (lane == 0 ? readlane_d(Eprev_first, kWave - 1) : before);
     }
     if (lane < n) {
       if (Ec) __builtin_nontemporal_store(Ebuf, Ec + row_first + lane);
@@ -253,16 +254,19 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
   int it_base = a.it0 - kWave, draw_L = 0;
   double draw_lnu = 0.0;
 
-#ifdef HMC_UNROLL2
-#pragma unroll 2
-#endif
-  for (int it = a.it0; it < a.it1; ++it) {
-    const bool post = it >= a.wu;
+  // One iteration; POST (it >= warm_up) is a compile-time constant: the launch runs the warm-up
+  // iterations and the sampling iterations as two loops, so the per-iteration tests of `post`
+  // (row writes, tallies, thinning) fold away.
+  auto iteration = [&](auto post_c, int it) {
+    constexpr bool post = decltype(post_c)::value;
     const bool write_row = post && ((it == a.niter) || (phase == a.thin - 1));
-    // E_chain / dE_chain of this iteration parked in lane nbuf (flushed every 64 or at the end).
+    // E_chain / dE_chain of this iteration parked in lane nbuf (flushed every 64 or at the end);
+    // E (and Eprev) need only be valid in lane 63, where the DPP reductions leave them.
     // Parked rows are consecutive (row_first + lane).  With thin = 1 they are also consecutive
     // iterations, so dE = E(lane) - E(lane - 1) is formed at the flush (lane 0: the E before the
     // block) and only E is parked; otherwise dE is parked too.
+    // Eprev (the E of the previous iteration) is only needed for a block's first row when
+    // thin = 1: it is then refreshed at each flush instead of every iteration.
     // (the empty asm statements keep these uniform conditions as branches, not per-lane selects)
     if (write_row) {
       if (nbuf == 0) {
@@ -270,21 +274,20 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
         row_first = row;
         Eprev_first = Eprev;
       }
-      if (thin1) {
-        if (lane == nbuf) Ebuf = E0;
-      } else {
+      Ebuf = park_lane(Ebuf, E0, nbuf, bp63);
+      if (!thin1) {
         asm volatile("" ::: "memory");
-        if (lane == nbuf) {
-          Ebuf = E0;
-          dEbuf = E0 - Eprev;
-        }
+        dEbuf = park_lane(dEbuf, E0 - Eprev, nbuf, bp63);
       }
       if (++nbuf == kWave) {
         flush_E(kWave);
         nbuf = 0;
+        if (thin1) Eprev = E0;
       }
+      if (!thin1) Eprev = E0;
+    } else {
+      Eprev = E0;
     }
-    Eprev = E0;
 
     // trajectory length (:441) and MH log-uniform (:461): wave-uniform
     int L;
@@ -295,7 +298,7 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     } else {
       if (it - it_base >= kWave) {                       // lane l draws (L, u) of iteration it + l
         it_base = it;
-        const uint4 r = draw_block(kDrawSlot, (uint32_t)(it + lane), gc, a.k0, a.k1);
+        const uint4 r = draw_block_uc(kDrawSlot, (uint32_t)(it + lane), gc, a.k0, a.k1);
         draw_L = uniform_int(r.x, a.L_low, a.L_high);
         const double u = u53(r.z, r.w);
         draw_lnu = u > 0.0 ? fast_log(u) : -__builtin_inf();   // log(random()), :461
@@ -315,8 +318,10 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     }
 
     // L leapfrog steps (samplers.py:448 -> :831-839), scalar loop
+    // the start point's copy as an opaque move: the integrated q (not the copy) is then the value
+    // carried to the next iteration, and the back edge needs no moves
 #pragma unroll
-    for (int e = 0; e < 2 * K; ++e) qi[e] = q[e];
+    for (int e = 0; e < 2 * K; ++e) asm("v_mov_b64 %0, %1" : "=v"(qi[e]) : "v"(q[e]));
     if constexpr (EXACT) {
       double t[2 * K];
 #pragma unroll
@@ -342,7 +347,9 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
           capp[2 * (l + 1) + 1] = a.D > 1 ? q[1] : q[0];
         }
       }
-    } else if (L > 0) {
+    } else if (L > 0 && (K > 1 || lane < a.npairs)) {
+      // (K = 1: lanes past npairs hold q = p = 0 and sit the integration out with EXEC off --
+      // the kernel runs at the board power cap, and idle FP64 lanes cost power, not time)
       // FAST: consecutive half kicks merged into one full kick, in shifted coordinates
       // u = q - q0 (2 FMA per coordinate per step instead of 3; same integrator, other rounding)
       // (without q0 the shift is the identity: integrate q in place, no copies in and out)
@@ -483,7 +490,9 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
 #endif
           m0l = m1l;
         }
-        E0 = FASTID ? __builtin_fma(wave_sum_dpp(m0l + kn), 0.5, hlogc) : 0.5 * (a.logc + wave_sum_dpp(m0l + kn));
+        // FASTID: E0 stays in lane 63 (the test, the park and Eprev read it there)
+        E0 = FASTID ? __builtin_fma(wave_sum_dpp_l63(m0l + kn), 0.5, hlogc)
+                    : 0.5 * (a.logc + wave_sum_dpp(m0l + kn));
       }
     }
     if (post && ++phase == a.thin) {
@@ -491,15 +500,20 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
       ++row;
       if (++qslot == a.Lq) qslot = 0;
     }
-  }
+  };
+  const int it_mid = min(max(a.wu, a.it0), a.it1);
+  for (int it = a.it0; it < it_mid; ++it) iteration(std::false_type{}, it);
+  for (int it = it_mid; it < a.it1; ++it) iteration(std::true_type{}, it);
+  // E of the launch's last iteration (E0 is not advanced past it)
+  if (a.it1 > a.it0) Eprev = E0;
 
   // flush parked E/dE, write back state and counters
   if (nbuf > 0) flush_E(nbuf);
 #pragma unroll
   for (int j = 0; j < K; ++j)
     if (pv[j]) store_pair(qrow, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);
+  if (lane == kWave - 1) a.Eprev[c] = Eprev;          // lane 63: where FASTID keeps E
   if (lane == 0) {
-    a.Eprev[c] = Eprev;
     if (a.cnt) {   // per-wave counts into one of HMC_COUNTER_SLOTS rows (no single-address hot spot)
       unsigned long long* cs = a.cnt + (c & (HMC_COUNTER_SLOTS - 1)) * HMC_NCOUNTERS;
       if (n_acc) atomicAdd(cs + HMC_CNT_ACCEPT, (unsigned long long)n_acc);
