@@ -389,12 +389,21 @@ void k_nuts_iters(RandArgs a) {
     // ================= one leapfrog for every chain inside a sub-tree (:612-614, :639)
     // chains outside a sub-tree are frozen by the EXEC mask of a divergent block (no per-dim
     // selects); the MFMAs and the reductions run with all lanes
+    // The last U-turn check of an even point m is against point m - 1 (check_points(m) ends with
+    // m - 1), which is the point in registers before this leapfrog: dq = q_m - q_{m-1} (the same
+    // subtraction the saved-vector check would do) and B = dq.p_{m-1} are formed here, A = dq.p_m
+    // after the second half kick, so that check loads nothing and points l = 3 (mod 4), which
+    // check_points only names at m = l + 1, are never saved.
     const bool act = state == S_READY;
+    double dq[M], regB = 0.0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) dq[m] = 0.0;
     if (act) {
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         const int dd = h + 4 * m;
         const double dt = dim_dt<MT, GEN>(a, dd), mi = dim_minv<MT, GEN>(a, dd);
+        const double pk = p[m], qk = q[m];
         if constexpr (EXACT) {
           p[m] = p[m] - (dt * (mi * gval<MT>(acc, m))) * 0.5;
           q[m] = q[m] + dt * p[m];
@@ -402,6 +411,8 @@ void k_nuts_iters(RandArgs a) {
           p[m] = __builtin_fma(-0.5 * dt * mi, gval<MT>(acc, m), p[m]);
           q[m] = __builtin_fma(dt, p[m], q[m]);
         }
+        dq[m] = q[m] - qk;
+        regB = mac<EXACT>(regB, dq[m], pk);
         if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -416,7 +427,9 @@ void k_nuts_iters(RandArgs a) {
         if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
     }
-    double mp1 = 0.0, kp1 = 0.0;
+    double mp1 = 0.0, kp1 = 0.0, regA = 0.0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) regA = mac<EXACT>(regA, dq[m], p[m]);
     if constexpr (MASS) {                               // x.P.x and p.inv(cov_p).p (acc holds the kick)
       double xv[M];
       d4 t[MT];
@@ -465,7 +478,7 @@ void k_nuts_iters(RandArgs a) {
       if (fabs(E_tmp - E_init) > 1000.0) {              // :647-651
         reject = true;
         if (h == 0) ++n_unst;
-      } else if ((mpt & 1) == 1) {                      // odd point: save (:654-658)
+      } else if ((mpt & 3) == 1) {                      // odd point: save (:654-658); 3 (mod 4): see dq
         const int s = save_slot(mpt, a.d_max);
         vstore<M>(W, V_SLOTS, 2 * s, q);
         vstore<M>(W, V_SLOTS + 1, 2 * s, p);
@@ -473,9 +486,14 @@ void k_nuts_iters(RandArgs a) {
     }
     // even point: sub-tree U-turn checks against check_points(mpt) (:699-736), converged loop
     const bool checking = later && !reject && (mpt & 1) == 0;
-    const int ncheck = checking ? cp_count(mpt) : 0;
+    {                                                   // the check against point mpt - 1, from registers
+      const double r_dot = chain_sum4(udir == 0 ? regA : regB);
+      const double l_dot = chain_sum4(udir == 0 ? regB : regA);
+      if (checking && l_dot < 0.0 && r_dot < 0.0) reject = true;
+    }
+    const int ncheck = checking && !reject ? cp_count(mpt) - 1 : 0;   // the saved check points
     const int ncheck_w = wave_max_i32(ncheck);
-    bool alive_chk = checking;
+    bool alive_chk = ncheck > 0;
     // check points of mpt, incrementally (cp_point): mpt - r + 1, then + r/2, + r/4, ...
     int cp_half = checking ? cp_r(mpt) : 2;
     int cp_pt = mpt - cp_half + 1;
