@@ -49,7 +49,7 @@ def parse(argv=None):
     ap.add_argument("--dim", type=int, default=100)
     ap.add_argument("--iters-per-step", type=int, default=0,
                     help="HMC iterations fused into one launch (= one timed step); 0 = auto: 40 for the Random "
-                         "sampler (HMC_sampler.gen_sample fuses a whole run into one launch), 2 for NUTS")
+                         "sampler (HMC_sampler.gen_sample fuses a whole run into one launch), 8 for NUTS")
     ap.add_argument("--chain-budget-gb", type=float, default=100.0,
                     help="HBM for the circular q_chain window of the timed launches (per GPU)")
     ap.add_argument("--fp-mode", default="fast", choices=["fast", "exact"])
@@ -257,7 +257,7 @@ def main():
     nuts = a.sampler == "nuts"
     D = a.dim
     offset, N = shard(a.chains, world, rank)
-    S = a.iters_per_step if a.iters_per_step > 0 else (2 if nuts else (20 if a.stream_diag else 40))
+    S = a.iters_per_step if a.iters_per_step > 0 else (8 if nuts else (20 if a.stream_diag else 40))
     W, K = a.warmup, a.steps
     feed_steps = a.stream_feed if a.stream_feed > 0 else max(1, 60 // S)
     n_iter = (W + K) * S
@@ -315,6 +315,8 @@ def main():
     c1 = eng.read_counters()
     lf_local = int(c1[H.CNT_LEAPFROG] - c0[H.CNT_LEAPFROG])
     acc = int(c1[H.CNT_ACCEPT] - c0[H.CNT_ACCEPT])
+    if a.sampler == "nuts" and c1[H.CNT_ACCEPT] > 0:   # NUTS uses this slot for chain hand-off give-ups
+        raise RuntimeError("NUTS kernel: %d chain hand-offs timed out" % c1[H.CNT_ACCEPT])
     dmax_hits = int(c1[H.CNT_DMAX] - c0[H.CNT_DMAX])
     wave_steps = int(c1[H.CNT_LEAPFROG_SQ] - c0[H.CNT_LEAPFROG_SQ])   # NUTS: steps of 16-chain waves
     tot = torch.tensor([float(lf_local), float(acc), float(dmax_hits), elapsed, kern_ms], dtype=torch.float64,

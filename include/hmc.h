@@ -44,7 +44,8 @@ enum { HMC_MODE_EXACT = 0, HMC_MODE_FAST = 1 };
 
 /* counters[] slots (unsigned long long, device, accumulated with atomics) */
 enum {
-  HMC_CNT_ACCEPT = 0,        /* accepted proposals, i >= warm_up (samplers.py:467)          */
+  HMC_CNT_ACCEPT = 0,        /* accepted proposals, i >= warm_up (samplers.py:467); NUTS:
+                                chain hand-offs between slots given up (a launch error, 0)   */
   HMC_CNT_ACCEPT_WU = 1,     /* accepted proposals, i <  warm_up (samplers.py:469)          */
   HMC_CNT_LEAPFROG = 2,      /* sum of L actually integrated (the metric's unit of work)     */
   HMC_CNT_LEAPFROG_SQ = 3,   /* Random: sum of L^2 (N_total_steps, Q13); NUTS: wave steps    */

@@ -34,11 +34,35 @@ namespace {
 #endif
 constexpr int kNutsWaves = HMC_NUTS_WAVES;
 
-// S_FETCH: the chain slot takes the next chain of the launch from the queue (or retires);
-// S_GRAD: a fetched chain waits one wave step for the MFMA gradient at its start point.
-// S_SUB_LOAD: a doubling in the direction opposite to the last sub-tree loads that end first.
+// S_FETCH: the chain slot hands its chain back and takes the next (chain, iteration) unit of the
+// launch from the queue (or retires); S_WAIT: the unit's chain is still finishing its previous
+// iteration in another slot; S_GRAD: a fetched chain waits one wave step for the MFMA gradient at
+// its start point.  S_SUB_LOAD: a doubling in the direction opposite to the last sub-tree loads
+// that end first.
 enum : int { S_ITER_START = 0, S_SUB_START = 1, S_READY = 2, S_ITER_END = 3, S_DONE = 4, S_FETCH = 5, S_GRAD = 6,
-             S_SUB_LOAD = 7 };
+             S_SUB_LOAD = 7, S_WAIT = 8 };
+
+// Chain hand-off between slots (any CU, any XCD) inside a launch: the chain's state (q, E_prev, tape
+// cursor) is stored write-through (relaxed agent-scope atomic stores, sc1) and drained
+// (vmcnt(0)) before one lane publishes the chain's iteration count with a relaxed agent-scope
+// store; the taking slot polls that word and reads the state with sc1 loads, which bypass its
+// CU's L1 (cdna_hip_programming.md Guideline 16, R1).
+template <typename T>
+__device__ __forceinline__ void st_wt(T* p, T x) { __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <typename T>
+__device__ __forceinline__ T ld_wt(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt_d(double* p, double x) {
+  st_wt(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, x));
+}
+__device__ __forceinline__ double ld_wt_d(const double* p) {
+  return __builtin_bit_cast(double, ld_wt(reinterpret_cast<const unsigned long long*>(p)));
+}
+
+// waves steps a slot may wait for a chain's previous iteration before the launch gives up (the
+// holder always advances, so this is only a guard against a broken hand-off)
+constexpr unsigned kMaxWaitSteps = 1u << 20;
 
 // workspace vector ids (per chain).  The live points old/new (:577, :623, :750, :775) are two
 // buffer pairs, (0, 1) and (2, 3): `old2` (0 or 2, per chain) names the old pair and the other is
@@ -47,6 +71,10 @@ enum : int { V_OLD_Q = 0, V_OLD_G = 1, V_NEW_Q = 2, V_NEW_G = 3, V_LEFT_Q = 4, V
              V_RIGHT_Q = 7, V_RIGHT_P = 8, V_RIGHT_G = 9, V_SLOTS = 10 };
 
 __device__ __forceinline__ int nuts_nvec(int d_max) { return V_SLOTS + 2 * (d_max + 1); }
+
+// bytes of the work queue block, zeroed before every launch: head, a spare word, done[n] (u32),
+// padded to a multiple of 16
+inline size_t nuts_queue_bytes(int64_t n) { return (size_t)((16 + 4 * n + 15) / 16 * 16); }
 
 // Workspace: per chain slot, nvec vectors of Dp = 4M doubles (dims, zero padded), slot-contiguous,
 // the 16 slots of a wave in one block addressed through a wave-uniform buffer descriptor (SGPR
@@ -180,11 +208,12 @@ void k_nuts_iters(RandArgs a) {
 
   const int lane = threadIdx.x & (kWave - 1);
   const int h = lane >> 4;
-  // Persistent waves with a chain queue: each of the 16 chain slots of a wave takes chains from a
-  // launch-wide counter and, when a chain has done its iterations, writes it back and takes the
-  // next one.  Slots no longer idle while the slowest tree of a fixed 16-chain group finishes
-  // (lane utilisation).  Draws are keyed by the chain, so results do not depend on which slot or
-  // wave runs it.  The tree vectors are per slot (W), the tape cursors per chain.
+  // Persistent waves with a work queue: each of the 16 chain slots of a wave takes (chain,
+  // iteration) units from a launch-wide counter, unit u = iteration it0 + u / n of chain u % n, and
+  // hands the chain back after that one iteration (one tree).  Slots idle only while the last
+  // trees of the launch finish, not the last chains' remaining iterations (lane utilisation).
+  // Draws are keyed by (chain, iteration), so results do not depend on which slot or wave runs a
+  // tree.  The tree vectors are per slot (W), the tape cursors and hand-off words per chain.
   const int64_t wv = (int64_t)blockIdx.x * kNutsWaves + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int64_t wave_doubles = (int64_t)nuts_nvec(a.d_max) * M * kWave;
   const int64_t n_waves = (a.n + 15) / 16;
@@ -192,6 +221,9 @@ void k_nuts_iters(RandArgs a) {
                  (lane & 15) * nuts_nvec(a.d_max) * (4 * M * 8) + h * 16};
   int64_t* const tcur = reinterpret_cast<int64_t*>(a.ws + n_waves * wave_doubles);
   unsigned long long* const queue = reinterpret_cast<unsigned long long*>(tcur + n_waves * 16);   // zeroed per launch
+  unsigned* const done = reinterpret_cast<unsigned*>(queue + 2);    // per chain: iterations done (zeroed per launch)
+  const unsigned long long n_units = (unsigned long long)a.n * (unsigned long long)(a.it1 - a.it0);
+  unsigned waited = 0;
   int64_t c = 0;
   bool live = false;
   uint64_t gc = 0;
@@ -212,7 +244,7 @@ void k_nuts_iters(RandArgs a) {
   double E_init = 0.0, E_max_now = 0.0, E_max_old = 0.0, pi_new = 1.0, pi_old = 1.0;
   int64_t tpos = 0;                                     // replay tape cursor (persists across launches)
   int old2 = 0;                                         // vector offset of the live_point_old pair
-  unsigned long long n_lf = 0, n_unst = 0, n_dmax = 0, n_tape = 0, n_steps = 0;
+  unsigned long long n_lf = 0, n_unst = 0, n_dmax = 0, n_tape = 0, n_steps = 0, n_giveup = 0;
 
   auto draw = [&](bool direction) -> double {           // next random number of this chain (reference order)
     if constexpr (REPLAY) {
@@ -243,40 +275,59 @@ void k_nuts_iters(RandArgs a) {
             if (h + 4 * m < a.D) rowp[h + 4 * m] = q[m];
         }
         Eprev = E_init;
-        ++it;
-        state = it < a.it1 ? S_ITER_START : S_FETCH;
+        state = S_FETCH;                                // hand the chain back after each tree
       }
-      if (state == S_FETCH && live) {                   // chain done: write back its state
+      if (state == S_FETCH && live) {                   // tree done: write the chain's state through
 #pragma unroll
         for (int m = 0; m < M; ++m) {
           const int dd = h + 4 * m;
-          if (dd < a.D) a.q[c * a.D + dd] = q[m];
+          if (dd < a.D) st_wt_d(a.q + c * a.D + dd, q[m]);
         }
-        if (h == 0) a.Eprev[c] = Eprev;
-        if (REPLAY && h == 0) tcur[c] = tpos;
-        live = false;
+        if (h == 0) st_wt_d(a.Eprev + c, Eprev);
+        if (REPLAY && h == 0) st_wt(tcur + c, tpos);
       }
-      {                                                 // next chain from the queue (converged shuffle)
+      if (__builtin_amdgcn_ballot_w64(state == S_FETCH && live)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the state has reached L2/memory ...
+        if (state == S_FETCH && live && h == 0) st_wt(done + c, (unsigned)(it + 1 - a.it0));   // ... then publish
+        if (state == S_FETCH) live = false;
+      }
+      {                                                 // next unit from the queue (converged shuffle)
         const bool fetching = state == S_FETCH;
-        long long nc = (fetching && h == 0) ? (long long)atomicAdd(queue, 1ull) : 0ll;
-        nc = __shfl(nc, lane & 15, kWave);
+        unsigned long long u = (fetching && h == 0) ? atomicAdd(queue, 1ull) : 0ull;
+        u = __shfl(u, lane & 15, kWave);
         if (fetching) {
-          if (nc < a.n) {
-            c = nc;
-            live = true;
+          if (u < n_units) {
+            c = (int64_t)(u % (unsigned long long)a.n);
+            it = a.it0 + (int)(u / (unsigned long long)a.n);
             gc = (uint64_t)(a.chain_offset + c);
-#pragma unroll
-            for (int m = 0; m < M; ++m) {
-              const int dd = h + 4 * m;
-              q[m] = dd < a.D ? a.q[c * a.D + dd] : 0.0;
-            }
-            Eprev = a.Eprev[c];
-            tpos = REPLAY ? tcur[c] : 0;
-            it = a.it0;
-            state = S_GRAD;                             // gradient at q in the next wave step
+            waited = 0;
+            state = S_WAIT;
           } else {
             state = S_DONE;
           }
+        }
+      }
+      if (state == S_WAIT) {                            // the chain's previous iteration published?
+        const unsigned need = (unsigned)(it - a.it0);
+        bool ready = need == 0;
+        if (!ready) {
+          ready = ld_wt(done + c) >= need;
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the state loads below the poll
+          if (!ready && ++waited > kMaxWaitSteps) {   // broken hand-off: flag it and retire the slot
+            ++n_giveup;
+            state = S_DONE;
+          }
+        }
+        if (ready) {
+          live = true;
+#pragma unroll
+          for (int m = 0; m < M; ++m) {
+            const int dd = h + 4 * m;
+            q[m] = dd < a.D ? ld_wt_d(a.q + c * a.D + dd) : 0.0;
+          }
+          Eprev = ld_wt_d(a.Eprev + c);
+          tpos = REPLAY ? ld_wt(tcur + c) : 0;
+          state = S_GRAD;                               // gradient at q in the next wave step
         }
       }
       const bool starting = state == S_ITER_START;
@@ -611,6 +662,7 @@ void k_nuts_iters(RandArgs a) {
   n_unst = wave_sum_u64(n_unst);
   n_dmax = wave_sum_u64(h == 0 ? n_dmax : 0ull);
   n_tape = wave_sum_u64(h == 0 ? n_tape : 0ull);
+  n_giveup = wave_sum_u64(h == 0 ? n_giveup : 0ull);
   if (lane == 0 && a.cnt) {
     unsigned long long* cs = a.cnt + (wv & (HMC_COUNTER_SLOTS - 1)) * HMC_NCOUNTERS;
     if (n_lf) {
@@ -620,6 +672,7 @@ void k_nuts_iters(RandArgs a) {
     if (n_unst) atomicAdd(cs + HMC_CNT_UNSTABLE, n_unst);
     if (n_dmax) atomicAdd(cs + HMC_CNT_DMAX, n_dmax);
     if (n_tape) atomicAdd(cs + HMC_CNT_OOB_REJECT, n_tape);   // NUTS: replay tape exhausted
+    if (n_giveup) atomicAdd(cs + HMC_CNT_ACCEPT, n_giveup);    // NUTS: chain hand-offs given up (must be 0)
     atomicAdd(cs + HMC_CNT_LEAPFROG_SQ, n_steps);               // NUTS: wave steps (lane utilisation)
   }
 }
@@ -631,8 +684,8 @@ hipError_t launch_nuts_mt2(const RandArgs& a, bool gen, bool replay, hipStream_t
   const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)device_cus())));
   const int64_t n_waves = (a.n + 15) / 16;
   const int64_t wave_doubles = (int64_t)(V_SLOTS + 2 * (a.d_max + 1)) * 4 * MT * kWave;
-  double* queue = a.ws + n_waves * wave_doubles + n_waves * 16;
-  if (hipError_t e = hipMemsetAsync(queue, 0, sizeof(unsigned long long), s)) return e;
+  double* queue = a.ws + n_waves * wave_doubles + n_waves * 16;   // queue head, (unused), done[n]
+  if (hipError_t e = hipMemsetAsync(queue, 0, nuts_queue_bytes(a.n), s)) return e;
   const size_t lds = (size_t)MT * 4 * MT * kWave * sizeof(double);
   if (a.minvf) {
     if (replay) k_nuts_iters<MT, EXACT, true, true, true><<<grid, 64 * kNutsWaves, lds, s>>>(a);
@@ -657,7 +710,8 @@ hipError_t launch_nuts_mt(const RandArgs& a, bool exact, bool gen, bool replay, 
 int64_t nuts_ws_doubles(int64_t n, int D, int d_max) {
   const int MT = dense_tiles(D);
   const int64_t waves = (n + 15) / 16;
-  return waves * (int64_t)(V_SLOTS + 2 * (d_max + 1)) * 4 * MT * kWave + waves * 16 + 1;   // vectors + tape cursors + chain queue
+  // vectors + tape cursors + work queue (head, spare, per-chain iterations done)
+  return waves * (int64_t)(V_SLOTS + 2 * (d_max + 1)) * 4 * MT * kWave + waves * 16 + nuts_queue_bytes(n) / 8;
 }
 
 hipError_t launch_nuts_iters(const RandArgs& a, bool exact, bool replay, hipStream_t s) {
