@@ -50,10 +50,24 @@ struct FragReader {
   __device__ __forceinline__ double operator()(int f) const { return f < 128 ? lo[f * kWave] : hi[(f - 128) * kWave]; }
 };
 
+// Short last tile: when the last 16-row output tile holds at most 4 dims (D = 97..100 at MT = 7),
+// its rows are computed by v_mfma_f64_4x4x4f64 (4 blocks, a quarter of the 16x16x4 cost) instead
+// of a 16x16x4 MFMA that is 3/4 zero rows.  Lane maps of the 4-block instruction (probed on
+// gfx950, scripts/ubench/mfma_f64_4x4_layout.hip): A lane l = (k = l>>4, block = (l>>2)&3,
+// i = l&3), B lane l = (k = l>>4, block = (l>>2)&3, j = l&3), D lane l = (i = l>>4,
+// block = (l>>2)&3, j = l&3).  With block b = chains 4b..4b+3, B is the tile's usual x operand
+// (lane (c, h) holds dim 4ks + h of chain c), A is P[16(MT-1) + (l&3)][4ks + (l>>4)] (staged that
+// way, replicated over the blocks), and lane (c, h) receives row 16(MT-1) + h of chain c: the
+// element the 16x16x4 layout puts in acc[MT-1][0].
+// SHORT = false keeps the 16x16x4 form (the NUTS kernel: its runtime branch per k-step cost more
+// than the saved MFMA cycles there, -2.6%; the dense Random kernel gains +3%).
+template <int MT, bool SHORT = true>
+__device__ __forceinline__ bool short_last_tile(int D) { return SHORT && D <= 16 * (MT - 1) + 4; }
+
 // DB: fragments of the next k-step read while this one's MFMAs run (one wave per SIMD must hide
 // the LDS latency itself); without it the reads sit right before their MFMAs and a second wave
 // on the SIMD covers the latency, for MT fewer live registers.
-template <int MT, bool GEN, bool DB = true>
+template <int MT, bool GEN, bool DB = true, bool SHORT = true>
 __device__ __forceinline__ void gradient(const DenseArgs& a, const double* __restrict__ sP, int lane, int h,
                                          const double (&q)[4 * MT], d4 (&acc)[MT]) {
   // k-step ks: MT MFMAs (one per 16-dim output tile) with the P fragments of ks, while the
@@ -66,7 +80,13 @@ __device__ __forceinline__ void gradient(const DenseArgs& a, const double* __res
   // skipped (D = 100: 25 of 28 k-steps).  Only the last three k-steps can be padding, so only
   // they carry the (scalar) exit test.
   const int ks_end = __builtin_amdgcn_readfirstlane((a.D + 3) >> 2);
+  const bool sl = short_last_tile<MT, SHORT>(a.D);      // uniform
+  double a4 = 0.0;                                      // the short last tile's accumulator
   const FragReader frag(sP, lane);
+  auto mfma = [&](int nt, double af, double x) {
+    if (nt == MT - 1 && sl) a4 = __builtin_amdgcn_mfma_f64_4x4x4f64(af, x, a4, 0, 0, 0);
+    else acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, x, acc[nt], 0, 0, 0);
+  };
   if constexpr (!DB) {
 #pragma unroll
     for (int nt = 0; nt < MT; ++nt) acc[nt] = d4{0.0, 0.0, 0.0, 0.0};
@@ -78,9 +98,10 @@ __device__ __forceinline__ void gradient(const DenseArgs& a, const double* __res
       for (int nt = 0; nt < MT; ++nt) af[nt] = frag(nt * KS + ks);
       const double x = (GEN && a.q0) ? q[ks] - a.q0[min(h + 4 * ks, a.D - 1)] : q[ks];
 #pragma unroll
-      for (int nt = 0; nt < MT; ++nt) acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[nt], x, acc[nt], 0, 0, 0);
+      for (int nt = 0; nt < MT; ++nt) mfma(nt, af[nt], x);
       __builtin_amdgcn_sched_barrier(0);
     }
+    if (sl) acc[MT - 1] = d4{a4, 0.0, 0.0, 0.0};
     return;
   }
   double af[MT], an[MT];
@@ -103,11 +124,12 @@ __device__ __forceinline__ void gradient(const DenseArgs& a, const double* __res
     // padded dims (d >= D) meet zero columns of P, so no guard is needed here
     const double x = (GEN && a.q0) ? q[ks] - a.q0[min(h + 4 * ks, a.D - 1)] : q[ks];
 #pragma unroll
-    for (int nt = 0; nt < MT; ++nt) acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[nt], x, acc[nt], 0, 0, 0);
+    for (int nt = 0; nt < MT; ++nt) mfma(nt, af[nt], x);
 #pragma unroll
     for (int nt = 0; nt < MT; ++nt) af[nt] = an[nt];
     __builtin_amdgcn_sched_barrier(0);
   }
+  if (sl) acc[MT - 1] = d4{a4, 0.0, 0.0, 0.0};
 }
 
 // y = M x for a symmetric (or pre-transposed) row-major D x D matrix in global memory (L2-resident),
@@ -171,16 +193,17 @@ __device__ __forceinline__ double dim_dt(const DenseArgs& a, int d) {
 
 
 // P fragments -> LDS (zero padded): fragment (nt, ks) lane l holds P[16nt + (l&15)][4ks + (l>>4)],
-// stored lane-linear so every MFMA A-operand read is one conflict-free ds_read_b64.
+// stored lane-linear so every MFMA A-operand read is one conflict-free ds_read_b64.  A short last
+// tile (short_last_tile) holds P[16nt + (l&3)][4ks + (l>>4)] instead: the 4x4x4 A operand.
 // With a dense mass matrix the staged matrix is the kick matrix inv(cov_p).prec (a.kick).
-template <int MT>
+template <int MT, bool SHORT = true>
 __device__ __forceinline__ void stage_precision(const DenseArgs& a, double* sP) {
   constexpr int KS = 4 * MT;
   const double* src = a.kick ? a.kick : a.prec;
   for (int f = threadIdx.x; f < MT * KS * kWave; f += blockDim.x) {
     const int l = f & (kWave - 1), t = f / kWave;
     const int nt = t / KS, ks = t - nt * KS;
-    const int n = 16 * nt + (l & 15), k = 4 * ks + (l >> 4);
+    const int n = 16 * nt + ((nt == MT - 1 && short_last_tile<MT, SHORT>(a.D)) ? (l & 3) : (l & 15)), k = 4 * ks + (l >> 4);
     sP[f] = (n < a.D && k < a.D) ? src[(int64_t)n * a.D + k] : 0.0;
   }
   __syncthreads();

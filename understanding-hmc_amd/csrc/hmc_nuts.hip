@@ -204,7 +204,7 @@ __global__ __launch_bounds__(64 * kNutsWaves) __attribute__((amdgpu_waves_per_eu
 void k_nuts_iters(RandArgs a) {
   constexpr int M = 4 * MT;
   extern __shared__ double sP[];
-  stage_precision<MT>(a, sP);
+  stage_precision<MT, false>(a, sP);
 
   const int lane = threadIdx.x & (kWave - 1);
   const int h = lane >> 4;
@@ -467,7 +467,7 @@ void k_nuts_iters(RandArgs a) {
         if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
     }
-    gradient<MT, GEN>(a, sP, lane, h, q, acc);
+    gradient<MT, GEN, true, false>(a, sP, lane, h, q, acc);
     if (act) {
 #pragma unroll
       for (int m = 0; m < M; ++m) {
