@@ -59,15 +59,19 @@ struct FragReader {
 // (lane (c, h) holds dim 4ks + h of chain c), A is P[16(MT-1) + (l&3)][4ks + (l>>4)] (staged that
 // way, replicated over the blocks), and lane (c, h) receives row 16(MT-1) + h of chain c: the
 // element the 16x16x4 layout puts in acc[MT-1][0].
-// SHORT = false keeps the 16x16x4 form (the NUTS kernel: its runtime branch per k-step cost more
-// than the saved MFMA cycles there, -2.6%; the dense Random kernel gains +3%).
-template <int MT, bool SHORT = true>
-__device__ __forceinline__ bool short_last_tile(int D) { return SHORT && D <= 16 * (MT - 1) + 4; }
+// SHORT: kShortNever keeps the 16x16x4 form, kShortRuntime tests D per launch (one uniform branch
+// per k-step: +3% on the dense Random kernel, -2.6% on NUTS), kShortAlways is an instance compiled
+// for D = 16(MT-1)+1 .. 16(MT-1)+4 (no branch).
+enum : int { kShortNever = 0, kShortRuntime = 1, kShortAlways = 2 };
+template <int MT, int SHORT = kShortRuntime>
+__device__ __forceinline__ bool short_last_tile(int D) {
+  return SHORT == kShortAlways || (SHORT == kShortRuntime && D <= 16 * (MT - 1) + 4);
+}
 
 // DB: fragments of the next k-step read while this one's MFMAs run (one wave per SIMD must hide
 // the LDS latency itself); without it the reads sit right before their MFMAs and a second wave
 // on the SIMD covers the latency, for MT fewer live registers.
-template <int MT, bool GEN, bool DB = true, bool SHORT = true>
+template <int MT, bool GEN, bool DB = true, int SHORT = kShortRuntime>
 __device__ __forceinline__ void gradient(const DenseArgs& a, const double* __restrict__ sP, int lane, int h,
                                          const double (&q)[4 * MT], d4 (&acc)[MT]) {
   // k-step ks: MT MFMAs (one per 16-dim output tile) with the P fragments of ks, while the
@@ -196,7 +200,7 @@ __device__ __forceinline__ double dim_dt(const DenseArgs& a, int d) {
 // stored lane-linear so every MFMA A-operand read is one conflict-free ds_read_b64.  A short last
 // tile (short_last_tile) holds P[16nt + (l&3)][4ks + (l>>4)] instead: the 4x4x4 A operand.
 // With a dense mass matrix the staged matrix is the kick matrix inv(cov_p).prec (a.kick).
-template <int MT, bool SHORT = true>
+template <int MT, int SHORT = kShortRuntime>
 __device__ __forceinline__ void stage_precision(const DenseArgs& a, double* sP) {
   constexpr int KS = 4 * MT;
   const double* src = a.kick ? a.kick : a.prec;

@@ -199,12 +199,14 @@ __device__ __forceinline__ double mac(double acc, double x, double y) {
 // MASS: full (non-diagonal) cov_p (implies GEN): LDS holds the kick matrix inv(cov_p).P
 // (stage_precision), p = C z, and every energy takes P x and inv(cov_p) p from two L2 products
 // (matvec_global) in converged code.  Its own instantiation, like the dense Random kernel's.
-template <int MT, bool EXACT, bool GEN, bool REPLAY, bool MASS = false>
+// SHORT: the gradient's short-last-tile form (hmc_dense_ops.hpp), compiled in (kShortAlways) for
+// the plain instances at D = 97..100.
+template <int MT, bool EXACT, bool GEN, bool REPLAY, bool MASS = false, int SHORT = kShortNever>
 __global__ __launch_bounds__(64 * kNutsWaves) __attribute__((amdgpu_waves_per_eu(kNutsWaves / 4, kNutsWaves / 4)))
 void k_nuts_iters(RandArgs a) {
   constexpr int M = 4 * MT;
   extern __shared__ double sP[];
-  stage_precision<MT, false>(a, sP);
+  stage_precision<MT, SHORT>(a, sP);
 
   const int lane = threadIdx.x & (kWave - 1);
   const int h = lane >> 4;
@@ -467,7 +469,7 @@ void k_nuts_iters(RandArgs a) {
         if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
     }
-    gradient<MT, GEN, true, false>(a, sP, lane, h, q, acc);
+    gradient<MT, GEN, true, SHORT>(a, sP, lane, h, q, acc);
     if (act) {
 #pragma unroll
       for (int m = 0; m < M; ++m) {
@@ -694,8 +696,18 @@ hipError_t launch_nuts_mt2(const RandArgs& a, bool gen, bool replay, hipStream_t
     if (replay) k_nuts_iters<MT, EXACT, true, true><<<grid, 64 * kNutsWaves, lds, s>>>(a);
     else k_nuts_iters<MT, EXACT, true, false><<<grid, 64 * kNutsWaves, lds, s>>>(a);
   } else {
-    if (replay) k_nuts_iters<MT, EXACT, false, true><<<grid, 64 * kNutsWaves, lds, s>>>(a);
-    else k_nuts_iters<MT, EXACT, false, false><<<grid, 64 * kNutsWaves, lds, s>>>(a);
+    bool done = false;
+    if constexpr (MT == 7) {
+      if (a.D <= 16 * (MT - 1) + 4) {                   // D = 97..100 (c5: D = 100)
+        if (replay) k_nuts_iters<MT, EXACT, false, true, false, kShortAlways><<<grid, 64 * kNutsWaves, lds, s>>>(a);
+        else k_nuts_iters<MT, EXACT, false, false, false, kShortAlways><<<grid, 64 * kNutsWaves, lds, s>>>(a);
+        done = true;
+      }
+    }
+    if (!done) {
+      if (replay) k_nuts_iters<MT, EXACT, false, true><<<grid, 64 * kNutsWaves, lds, s>>>(a);
+      else k_nuts_iters<MT, EXACT, false, false><<<grid, 64 * kNutsWaves, lds, s>>>(a);
+    }
   }
   return hipGetLastError();
 }
