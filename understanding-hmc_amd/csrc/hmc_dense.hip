@@ -43,14 +43,16 @@ constexpr bool kDenseDB = WAVES <= 4 || HMC_DENSE_DB;
 
 // MASS: dense (non-diagonal) mass matrix (implies GEN): its own instantiation, so the extra
 // products' registers never touch the diagonal-mass kernels.
-template <int MT, bool EXACT, bool GEN, bool REPLAY, int WAVES, bool MASS = false>
+// SHORT: the gradient's short-last-tile form (hmc_dense_ops.hpp): compiled in (kShortAlways) for
+// the plain instances at D = 97..100, tested per launch (kShortRuntime) in the others.
+template <int MT, bool EXACT, bool GEN, bool REPLAY, int WAVES, bool MASS = false, int SHORT = kShortRuntime>
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVES / 4, WAVES / 4)))
 void k_dense_iters(DenseArgs a) {
   constexpr int M = 4 * MT;
   extern __shared__ double sP[];
   __shared__ double s_ntab[REPLAY ? 2 : kNormalTableDoubles];   // Box–Muller tables (Philox momentum)
   if constexpr (!REPLAY) init_normal_tables(s_ntab);             // synchronised by stage_precision
-  stage_precision<MT>(a, sP);
+  stage_precision<MT, SHORT>(a, sP);
 
   const int lane = threadIdx.x & (kWave - 1);
   const int h = lane >> 4;
@@ -130,7 +132,7 @@ void k_dense_iters(DenseArgs a) {
     }
     // ---- gradient at q and E0 = V(q) + K(p)  (:434)
     if (!g_read || it != a.it0) {
-      gradient<MT, GEN, kDenseDB<WAVES>>(a, sP, lane, h, q, acc);
+      gradient<MT, GEN, kDenseDB<WAVES>, SHORT>(a, sP, lane, h, q, acc);
       if (gch && live) {              // keep the cache valid for rejections (q stays, so does g)
 #pragma unroll
         for (int m = 0; m < M; ++m)
@@ -220,7 +222,7 @@ void k_dense_iters(DenseArgs a) {
           if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
       }
-      gradient<MT, GEN, kDenseDB<WAVES>>(a, sP, lane, h, q, acc);
+      gradient<MT, GEN, kDenseDB<WAVES>, SHORT>(a, sP, lane, h, q, acc);
       if (act) {
 #pragma unroll
         for (int m = 0; m < M; ++m) {
@@ -447,8 +449,18 @@ void launch_dense_w(const DenseArgs& a, bool gen, bool replay, hipStream_t s) {
     if (replay) k_dense_iters<MT, EXACT, true, true, WAVES><<<grid, 64 * WAVES, lds, s>>>(a);
     else k_dense_iters<MT, EXACT, true, false, WAVES><<<grid, 64 * WAVES, lds, s>>>(a);
   } else {
-    if (replay) k_dense_iters<MT, EXACT, false, true, WAVES><<<grid, 64 * WAVES, lds, s>>>(a);
-    else k_dense_iters<MT, EXACT, false, false, WAVES><<<grid, 64 * WAVES, lds, s>>>(a);
+    bool done = false;
+    if constexpr (MT == 7) {
+      if (a.D <= 16 * (MT - 1) + 4) {                   // D = 97..100 (c3: D = 100)
+        if (replay) k_dense_iters<MT, EXACT, false, true, WAVES, false, kShortAlways><<<grid, 64 * WAVES, lds, s>>>(a);
+        else k_dense_iters<MT, EXACT, false, false, WAVES, false, kShortAlways><<<grid, 64 * WAVES, lds, s>>>(a);
+        done = true;
+      }
+    }
+    if (!done) {
+      if (replay) k_dense_iters<MT, EXACT, false, true, WAVES, false, kShortNever><<<grid, 64 * WAVES, lds, s>>>(a);
+      else k_dense_iters<MT, EXACT, false, false, WAVES, false, kShortNever><<<grid, 64 * WAVES, lds, s>>>(a);
+    }
   }
 }
 
