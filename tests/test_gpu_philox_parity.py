@@ -7,9 +7,10 @@ the host from the same counters and replayed through the oracle (oracle/hmc_orac
 restates samplers.py:387-491 / :495-808):
   * momentum: the table-driven Box-Muller normals the kernels draw, read back through the C-ABI
     debug entry hmc_rng_normals (same transform, same (slot, iteration, global chain) counter);
-    the initial momentum (iteration 0, samplers.py:415) and the NUTS momenta use the libm-free
-    Box-Muller of hmc_device.hpp::normal_pair, restated here with NumPy (agrees to ~4e-15 of the
-    radius, test_gpu_random.py::test_philox_normals_match_numpy_box_muller);
+    the initial momentum (iteration 0, samplers.py:415) uses the libm-free Box-Muller of
+    hmc_device.hpp::normal_pair, restated here with NumPy (agrees to ~4e-15 of the radius,
+    test_gpu_random.py::test_philox_normals_match_numpy_box_muller); the NUTS momenta use the
+    table transform too;
   * trajectory length L (samplers.py:441) and MH log-uniform (:461): Philox block
     (0x80000000, iteration, chain lo, chain hi): L = L_low + (x * (L_high - L_low)) >> 32,
     u = ((w << 21) | (z >> 11)) * 2^-53, log u (NumPy log; the kernel's fast_log is within 1 ulp);
@@ -255,7 +256,7 @@ def test_nuts_production_kernel_vs_oracle(fp_mode):
     h = HMC_sampler(D, None, None, Nchain=N, Niter=Niter, warm_up_num=wu, sampler_type="NUTS", dt=0.1, d_max=d_max,
                     target=MVNTarget(np.zeros(D), cov), rng="philox", seed=seed, fp_mode=fp_mode)
     h.gen_sample_NUTS(q_start, 0, False, on_dmax="break")
-    p0, P = dense_momenta(seed, N, D, Niter, table=False)
+    p0, P = dense_momenta(seed, N, D, Niter)
     ref = O.gen_sample_nuts(O.HMCCore(FastMVN(np.zeros(D), cov), 0.1), q_start, N, Niter, wu, 1, d_max,
                             PhiloxNutsDraws(seed, p0, P), on_dmax="break")
     assert h.n_leapfrog == ref["n_leapfrog"]

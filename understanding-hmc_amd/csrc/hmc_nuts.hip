@@ -206,6 +206,8 @@ __global__ __launch_bounds__(64 * kNutsWaves) __attribute__((amdgpu_waves_per_eu
 void k_nuts_iters(RandArgs a) {
   constexpr int M = 4 * MT;
   extern __shared__ double sP[];
+  __shared__ double s_ntab[REPLAY ? 2 : kNormalTableDoubles];   // Box–Muller tables (Philox momentum)
+  if constexpr (!REPLAY) init_normal_tables(s_ntab);             // synchronised by stage_precision
   stage_precision<MT, SHORT>(a, sP);
 
   const int lane = threadIdx.x & (kWave - 1);
@@ -350,7 +352,7 @@ void k_nuts_iters(RandArgs a) {
 #pragma unroll
           for (int m = 0; m < M; m += 2) {
             double z0, z1;
-            normal_pair(draw_block((uint32_t)(h + 4 * m), (uint32_t)it, gc, a.k0, a.k1), z0, z1);
+            normal_pair_tab(draw_block((uint32_t)(h + 4 * m), (uint32_t)it, gc, a.k0, a.k1), s_ntab, z0, z1);
             const int d0 = h + 4 * m, d1 = d0 + 4;
             if (GEN && a.pscale) {
               z0 *= a.pscale[min(d0, a.D - 1)];
@@ -589,8 +591,13 @@ void k_nuts_iters(RandArgs a) {
     if (later && !reject) {                             // progressive sampling (:743-751)
       const double E_max_prev = E_max_now;
       E_max_now = fmax(E_max_prev, E_tmp);
-      const double num = exp(-(E_tmp - E_max_now));
-      pi_new = num + exp(E_max_now - E_max_prev) * pi_new;
+      // exp(-(E_tmp - E_max_now)) and exp(E_max_now - E_max_prev): one argument is exactly 0
+      // (E_max_now is one of E_tmp, E_max_prev), so one exp and exp(0) = 1, as the reference
+      // (NaN energies give the same NaN r as the two exps)
+      const bool up = E_max_now != E_max_prev;
+      const double e = exp(up ? E_max_now - E_max_prev : -(E_tmp - E_max_now));
+      const double num = up ? 1.0 : e;
+      pi_new = num + (up ? e : 1.0) * pi_new;
       const double r = num / pi_new;
       if (draw(false) < r) {
         vstore<M>(W, V_OLD_Q, 2 - old2, q);
