@@ -37,10 +37,10 @@ constexpr int kNutsWaves = HMC_NUTS_WAVES;
 // S_FETCH: the chain slot hands its chain back and takes the next (chain, iteration) unit of the
 // launch from the queue (or retires); S_WAIT: the unit's chain is still finishing its previous
 // iteration in another slot; S_GRAD: a fetched chain waits one wave step for the MFMA gradient at
-// its start point.  S_SUB_LOAD: a doubling in the direction opposite to the last sub-tree loads
-// that end first.
+// its start point.  (A doubling towards the other end starts from that end's q, p, g, loaded at
+// the previous sub-tree's end for the termination check: no load state.)
 enum : int { S_ITER_START = 0, S_SUB_START = 1, S_READY = 2, S_ITER_END = 3, S_DONE = 4, S_FETCH = 5, S_GRAD = 6,
-             S_SUB_LOAD = 7, S_WAIT = 8 };
+             S_WAIT = 8 };
 
 // Chain hand-off between slots (any CU, any XCD) inside a launch: the chain's state (q, E_prev, tape
 // cursor) is stored write-through (relaxed agent-scope atomic stores, sc1) and drained
@@ -430,14 +430,6 @@ void k_nuts_iters(RandArgs a) {
         k = 0;
         state = S_READY;
       }
-      if (state == S_SUB_LOAD) {                        // a doubling towards the other end: load it
-        const int b = udir == 0 ? V_RIGHT_Q : V_LEFT_Q;
-        vload<M>(W, 0, b, q);
-        vload<M>(W, 1, b, p);
-        gload<MT>(W, 2, b, acc);
-        k = 0;
-        state = S_READY;
-      }
     }
     if (!__builtin_amdgcn_ballot_w64(state != S_DONE)) break;
 
@@ -610,8 +602,13 @@ void k_nuts_iters(RandArgs a) {
     if (act && reject) state = S_ITER_END;               // q = live_point_q_old (:649, :731)
 
     // ================= sub-tree end: boundary, biased acceptance, termination (:757-784)
-    double tr = 0.0, tl = 0.0;
+    // The other end (q, p, g) is loaded here for the termination dots; a next doubling towards it
+    // starts from these registers (no separate boundary-load step).  The chain sums run inside
+    // this divergent block: v_permlane16/32_swap pair lanes c, c^16, c^32 of the same chain, which
+    // are active together.
     if (sub_end) {
+      double oqv[M], opv[M];
+      d4 og[MT];
       const int b = udir == 0 ? V_RIGHT_Q : V_LEFT_Q;    // this end <- (q, p)
       vstore<M>(W, 0, b, q);
       vstore<M>(W, 1, b, p);
@@ -626,9 +623,9 @@ void k_nuts_iters(RandArgs a) {
         maha_old = maha_new;
       }
       const int o = udir == 0 ? V_LEFT_Q : V_RIGHT_Q;   // the other end
-      double oqv[M], opv[M];
       vload<M>(W, 0, o, oqv);
       vload<M>(W, 1, o, opv);
+      gload<MT>(W, 2, o, og);
       // A = (q - q_other).p, B = (q - q_other).p_other; (tr, tl) = (A, -B) forward, (-B, A)
       // backward: the reference's terms up to exact sign flips
       double tA = 0.0, tB = 0.0;
@@ -638,12 +635,9 @@ void k_nuts_iters(RandArgs a) {
         tA = mac<EXACT>(tA, Dq, p[m]);
         tB = mac<EXACT>(tB, Dq, opv[m]);
       }
-      tr = udir == 0 ? tA : -tB;
-      tl = udir == 0 ? -tB : tA;
-    }
-    tr = chain_sum4(tr);
-    tl = chain_sum4(tl);
-    if (sub_end) {                                      // :779-784 (Q10: stop when BOTH ends turn)
+      const double tr = chain_sum4(udir == 0 ? tA : -tB);
+      const double tl = chain_sum4(udir == 0 ? -tB : tA);
+      // :779-784 (Q10: stop when BOTH ends turn)
       rterm = tr < 0.0;
       lterm = tl < 0.0;
       ++d;
@@ -655,13 +649,18 @@ void k_nuts_iters(RandArgs a) {
       } else {                                          // next doubling: its direction (:608) now
         Lsub = 1 << d;
         const int nd = (int)draw(true);
-        if (nd == udir) {                               // same end: it is (q, p, acc) in registers
-          k = 0;
-          state = S_READY;
-        } else {
+        if (nd != udir) {                               // the other end, loaded above
           udir = nd;
-          state = S_SUB_LOAD;
-        }
+#pragma unroll
+          for (int m = 0; m < M; ++m) {
+            q[m] = oqv[m];
+            p[m] = opv[m];
+          }
+#pragma unroll
+          for (int nt = 0; nt < MT; ++nt) acc[nt] = og[nt];
+        }                                               // (same end: (q, p, acc) in registers)
+        k = 0;
+        state = S_READY;
       }
     }
   }
