@@ -65,8 +65,9 @@ __device__ __forceinline__ double ld_wt_d(const double* p) {
 constexpr unsigned kMaxWaitSteps = 1u << 20;
 
 // workspace vector ids (per chain).  The live points old/new (:577, :623, :750, :775) are two
-// buffer pairs, (0, 1) and (2, 3): `old2` (0 or 2, per chain) names the old pair and the other is
-// new, so accepting a sub-tree's point swaps the names instead of copying two vectors.
+// buffers, 0 and 2 (1 and 3 are unused since the per-tree queue: no gradient is kept with them):
+// `old2` (0 or 2, per chain) names the old one and the other is new, so accepting a sub-tree's
+// point swaps the names instead of copying a vector.
 enum : int { V_OLD_Q = 0, V_OLD_G = 1, V_NEW_Q = 2, V_NEW_G = 3, V_LEFT_Q = 4, V_LEFT_P = 5, V_LEFT_G = 6,
              V_RIGHT_Q = 7, V_RIGHT_P = 8, V_RIGHT_G = 9, V_SLOTS = 10 };
 
@@ -269,8 +270,9 @@ void k_nuts_iters(RandArgs a) {
     {
       const bool at_end = state == S_ITER_END;
       if (at_end) {                                     // samplers.py:786-791: q = live_point_q_old
-        vload<M>(W, V_OLD_Q, old2, q);
-        gload<MT>(W, V_OLD_G, old2, acc);
+        vload<M>(W, V_OLD_Q, old2, q);                  // its gradient: recomputed by the slot that
+                                                        // takes the chain next (S_GRAD), so the live
+                                                        // points keep no gradient vector
         const int qrow = (it - a.wu) / a.thin;
         if (write_row_of(it) && a.qc && qrow >= a.q_row0) {
           double* rowp = a.qc + (c * (int64_t)a.Lq + qrow % a.Lq) * a.D;
@@ -408,7 +410,6 @@ void k_nuts_iters(RandArgs a) {
           if (a.dEc) a.dEc[row] = E_init - Eprev;
         }
         vstore<M>(W, V_OLD_Q, old2, q);                 // live_point_q_old = q (:577)
-        gstore<MT>(W, V_OLD_G, old2, acc);
         vstore<M>(W, V_LEFT_Q, 0, q);                   // left = (q, -p), right = (q, p) (:581-584)
         gstore<MT>(W, V_LEFT_G, 0, acc);
         vstore<M>(W, V_RIGHT_Q, 0, q);
@@ -513,7 +514,6 @@ void k_nuts_iters(RandArgs a) {
     const bool first = act && k == 0, later = act && k > 0;
     if (first) {                                        // first point (:617-626)
       vstore<M>(W, V_OLD_Q, 2 - old2, q);               // live_point_new (the other buffer pair)
-      gstore<MT>(W, V_OLD_G, 2 - old2, acc);
       maha_new = maha_pt;
       E_max_now = E_tmp;
       pi_new = 1.0;
@@ -593,7 +593,6 @@ void k_nuts_iters(RandArgs a) {
       const double r = num / pi_new;
       if (draw(false) < r) {
         vstore<M>(W, V_OLD_Q, 2 - old2, q);
-        gstore<MT>(W, V_OLD_G, 2 - old2, acc);
         maha_new = maha_pt;
       }
       ++k;
