@@ -49,7 +49,7 @@ def parse(argv=None):
     ap.add_argument("--dim", type=int, default=100)
     ap.add_argument("--iters-per-step", type=int, default=0,
                     help="HMC iterations fused into one launch (= one timed step); 0 = auto: 40 for the Random "
-                         "sampler (HMC_sampler.gen_sample fuses a whole run into one launch), 8 for NUTS")
+                         "sampler (HMC_sampler.gen_sample fuses a whole run into one launch), 16 for NUTS")
     ap.add_argument("--chain-budget-gb", type=float, default=100.0,
                     help="HBM for the circular q_chain window of the timed launches (per GPU)")
     ap.add_argument("--fp-mode", default="fast", choices=["fast", "exact"])
@@ -257,7 +257,7 @@ def main():
     nuts = a.sampler == "nuts"
     D = a.dim
     offset, N = shard(a.chains, world, rank)
-    S = a.iters_per_step if a.iters_per_step > 0 else (8 if nuts else (20 if a.stream_diag else 40))
+    S = a.iters_per_step if a.iters_per_step > 0 else (16 if nuts else (20 if a.stream_diag else 40))
     W, K = a.warmup, a.steps
     feed_steps = a.stream_feed if a.stream_feed > 0 else max(1, 60 // S)
     n_iter = (W + K) * S
