@@ -7,8 +7,17 @@ BASELINE.json metric configuration: D=100 unit MVN at 1,048,576 chains in total,
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 --chains is the TOTAL over all ranks (default 1,048,576, the metric's "1M chains"); rank r takes a
-contiguous global chain range (Philox is keyed by the global chain id, so every chain's samples
-are the same at any N).  The total is fixed, so scaling over N is strong scaling.
+contiguous global chain range.  Philox draws AND start points are keyed by the global chain id, so
+every chain's samples are the same at any N: the N-GPU line is the same job as the 1-GPU line
+(strong scaling).  --chains-per-gpu instead fixes the work per GPU (weak scaling; config c4).
+
+--config picks a BASELINE.json configuration (explicit flags still override):
+    metric  D=100 unit MVN, 1,048,576 chains in total (the default; BASELINE.json's metric)
+    c1      case1-script.py shape: D=2 unit MVN, 10 chains, 1000 warm-up + 1000 timed iterations
+    c2      D=100 unit MVN, 65,536 chains
+    c3      D=100 rho=0.95 dense precision (MFMA gradient), 262,144 chains
+    c4      D=1000 unit MVN, 131,072 chains per GPU (1,048,576 on 8 GPUs), streaming R-hat/ESS
+    c5      NUTS, D=100 rho=0.95, 65,536 chains
 
 One step = ONE kernel launch of hmc_random_iters that advances every chain of this GPU by
 --iters-per-step HMC iterations (momentum resample, L ~ U{5..19} leapfrogs, Metropolis test, sample
@@ -39,13 +48,27 @@ METRIC_CHAINS = 1 << 20      # BASELINE.json metric: "D=100 MVN at 1M chains"
 DEBUG_ENV = ("HMC_DEBUG_ABLATE", "HMC_DEBUG_L", "HMC_DEBUG_STAMPS", "HMC_LIB_PATH", "HMC_AMD_LIB")
 
 
+PRESETS = {
+    "metric": dict(chains=METRIC_CHAINS, dim=100),
+    "c1": dict(chains=10, dim=2, iters_per_step=100, steps=10, warmup=10),
+    "c2": dict(chains=65536, dim=100),
+    "c3": dict(chains=262144, dim=100, rho=0.95),
+    "c4": dict(chains_per_gpu=131072, dim=1000, stream_diag=True),
+    "c5": dict(chains=65536, dim=100, rho=0.95, sampler="nuts", steps=5, warmup=1),
+}
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="metric", choices=sorted(PRESETS),
+                    help="BASELINE.json configuration preset (explicit flags override its values)")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--chains", type=int, default=METRIC_CHAINS,
                     help="chains in TOTAL, split over the ranks (default 1,048,576 = the metric's 1M chains)")
+    ap.add_argument("--chains-per-gpu", type=int, default=0,
+                    help="weak scaling: this many chains per rank (total = this x N); overrides --chains")
     ap.add_argument("--dim", type=int, default=100)
     ap.add_argument("--iters-per-step", type=int, default=0,
                     help="HMC iterations fused into one launch (= one timed step); 0 = auto: 40 for the Random "
@@ -71,10 +94,24 @@ def parse(argv=None):
                     help="--stream-diag: steps between diagnostics updates; 0 = auto: every ~60 iterations")
     ap.add_argument("--no-order-tiles", action="store_true",
                     help="dense targets: MFMA tiles in chain order instead of L-ordered tiles")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group of N > 1 runs: nccl (= RCCL over xGMI, one GPU per rank) or gloo "
+                         "(host-side collectives; lets a test run several ranks on one GPU)")
+    ap.add_argument("--no-telemetry", action="store_true", help="do not sample board power / shader clock")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / sharding check without a GPU: every rank joins a gloo group and reports "
                          "its global chain range; rank 0 prints them as one JSON line")
-    return ap.parse_args(argv)
+    pre, _ = ap.parse_known_args(argv)
+    ap.set_defaults(**PRESETS[pre.config])
+    a = ap.parse_args(argv)
+    return a
+
+
+def resolve_chains(a, world):
+    """Total chains of the job and whether the per-GPU work is fixed (weak scaling)."""
+    if a.chains_per_gpu > 0:
+        return a.chains_per_gpu * world, True
+    return a.chains, False
 
 
 # ------------------------------------------------------------------ launcher (--gpus N, no torchrun)
@@ -126,6 +163,7 @@ def _cpu_worker(args):
     tgt = O.MVNTarget(np.zeros(D), cov)
     core = O.HMCCore(tgt, 0.1)
     q_start = O.start_pts(np.zeros(D), 2 * np.eye(D), 1)
+    rnd = max(2, min(20, 2000 // D))       # iterations per round: D=1000 spends ~1 s per iteration
     lf = 0
     t0 = time.time()
     # rounds of iterations of the reference-equivalent engine until the budget is spent
@@ -133,7 +171,7 @@ def _cpu_worker(args):
         if sampler == "nuts":
             out = O.gen_sample_nuts(core, q_start, 1, 2, 0, 1, d_max, O.LiveDraws(D, np.eye(D)), on_dmax="break")
         else:
-            out = O.gen_sample_random(core, q_start, 1, 20, 0, 1, 5, 20, O.LiveDraws(D, np.eye(D)))
+            out = O.gen_sample_random(core, q_start, 1, rnd, 0, 1, 5, 20, O.LiveDraws(D, np.eye(D)))
         lf += out["n_leapfrog"]
         q_start = out["q_chain"][:, -1, :]
     return lf, time.time() - t0
@@ -205,13 +243,74 @@ def pmc_traffic(shape):
     return None
 
 
+class Telemetry:
+    """Board power and shader clock of this rank's GPU, sampled every `period` s by a host thread
+    (amdsmi: read-only sysfs/SMU metrics, no HIP calls) while the timed region runs."""
+
+    def __init__(self, index, period=0.01):
+        self.index, self.period = index, period
+        self.samples, self.error, self._th, self._stop = [], None, None, None
+
+    def start(self):
+        import threading
+        try:
+            import amdsmi as S
+            S.amdsmi_init(S.AmdSmiInitFlags.INIT_AMD_GPUS)
+            hs = S.amdsmi_get_processor_handles()
+            self._h = hs[min(self.index, len(hs) - 1)]
+            self._S = S
+            self._read()
+        except Exception as e:   # noqa: BLE001 (telemetry is optional: report why it is missing)
+            self.error = f"{type(e).__name__}: {e}"
+            return self
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._loop, daemon=True)
+        self._th.start()
+        return self
+
+    def _read(self):
+        S = self._S
+        pw = S.amdsmi_get_power_info(self._h)
+        ck = S.amdsmi_get_clock_info(self._h, S.AmdSmiClkType.GFX)
+        w = pw.get("current_socket_power")
+        if not isinstance(w, (int, float)):
+            w = pw.get("average_socket_power")
+        return (float(w) if isinstance(w, (int, float)) else None,
+                float(ck["clk"]) if isinstance(ck.get("clk"), (int, float)) else None)
+
+    def _loop(self):
+        while not self._stop.is_set():
+            try:
+                self.samples.append(self._read())
+            except Exception as e:   # noqa: BLE001
+                self.error = f"{type(e).__name__}: {e}"
+                return
+            self._stop.wait(self.period)
+
+    def stop(self):
+        if self._th is not None:
+            self._stop.set()
+            self._th.join()
+            try:
+                self._S.amdsmi_shut_down()
+            except Exception:   # noqa: BLE001
+                pass
+        w = [x[0] for x in self.samples if x[0] is not None]
+        c = [x[1] for x in self.samples if x[1] is not None]
+        return dict(power_W=float(np.mean(w)) if w else None, power_W_max=float(np.max(w)) if w else None,
+                    sclk_MHz=float(np.mean(c)) if c else None, sclk_MHz_min=float(np.min(c)) if c else None,
+                    samples=len(self.samples), source="amdsmi current_socket_power / GFX clock during the timed steps",
+                    error=self.error)
+
+
 def dry_run(a, world, rank):
     """The rank/offset logic of a real run, on CPU ranks (gloo): no GPU is touched."""
     import torch
     import torch.distributed as dist
     if world > 1:
         dist.init_process_group("gloo")
-    offset, count = shard(a.chains, world, rank)
+    total, weak = resolve_chains(a, world)
+    offset, count = shard(total, world, rank)
     mine = torch.tensor([rank, offset, count], dtype=torch.int64)
     got = [torch.zeros(3, dtype=torch.int64) for _ in range(world)]
     if world > 1:
@@ -219,7 +318,8 @@ def dry_run(a, world, rank):
     else:
         got = [mine]
     if rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": world, "chains_total": a.chains,
+        print(json.dumps({"dry_run": True, "config": a.config, "n_gpus": world, "chains_total": total,
+                          "scaling": "weak" if weak else "strong", "dim": a.dim,
                           "shards": [[int(v) for v in g] for g in got]}), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -243,20 +343,33 @@ def main():
     import torch.distributed as dist
     if a.dry_run:
         return dry_run(a, world, rank)
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    # one GPU per rank; with fewer GPUs than ranks (a gloo test on a 1-GPU box) ranks share them
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
+    if world > 1:
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from hmc_amd.engine import NutsEngine, RandomEngine
     from hmc_amd.target import MVNTarget
     from hmc_amd import _lib as H
     from hmc_amd.diagnostics import StreamingDiagnostics, convergence_stats
+    from hmc_amd.utils import start_pts_device
+
+    def reduce(vals, op):
+        """Sum / max over ranks of a few host scalars."""
+        t = torch.tensor(vals, dtype=torch.float64)
+        if world > 1:
+            t = t.to(dev) if a.backend == "nccl" else t
+            dist.all_reduce(t, op=op)
+        return t.cpu().numpy().tolist()
 
     nuts = a.sampler == "nuts"
     D = a.dim
-    offset, N = shard(a.chains, world, rank)
+    chains_total, weak = resolve_chains(a, world)
+    offset, N = shard(chains_total, world, rank)
     S = a.iters_per_step if a.iters_per_step > 0 else (16 if nuts else (20 if a.stream_diag else 40))
     W, K = a.warmup, a.steps
     feed_steps = a.stream_feed if a.stream_feed > 0 else max(1, 60 // S)
@@ -264,7 +377,10 @@ def main():
     wu = W * S + 1                     # chain rows 0 .. K*S-1 are exactly the timed iterations
     timed_rows = K * S
     store = not (a.no_ess or a.stream_diag)
-    R = window_rows(timed_rows, int(a.chain_budget_gb * 1e9 // (8.0 * max(1, N) * D))) if store else 0
+    # window rows from the per-GPU budget of the 1-GPU job (strong scaling) so that every N keeps
+    # the same samples for R-hat / ESS; weak scaling: from this GPU's chains
+    ref_chains = N if weak else chains_total
+    R = window_rows(timed_rows, int(a.chain_budget_gb * 1e9 // (8.0 * max(1, ref_chains) * D))) if store else 0
     cov = np.eye(D) if a.rho == 0 else (np.diag(np.ones(D)) * (1 - a.rho) + a.rho)
     tgt = MVNTarget(np.zeros(D), cov)
     if nuts:
@@ -278,8 +394,8 @@ def main():
         window = torch.zeros((N, R, D), dtype=torch.float64, device=dev)
         eng.set_chain_window(window, 0)
     sd = StreamingDiagnostics(N, D, eng.L_chain - 1, tmax=a.tmax, device=dev) if a.stream_diag else None
-    rs = np.random.RandomState(a.seed + rank)
-    eng.init(torch.as_tensor(rs.standard_normal((N, D)) * np.sqrt(2.0), device=dev))
+    # starts ~ N(0, 2I) keyed by the GLOBAL chain id (utils.py:204-209): the same job at any N
+    eng.init(start_pts_device(a.seed, offset, N, D, scale=np.sqrt(2.0), device=dev))
     it = 1
     stream = torch.cuda.current_stream(dev)
 
@@ -299,9 +415,12 @@ def main():
     torch.cuda.synchronize(dev)
     c0 = eng.read_counters()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    tele = Telemetry(dev.index) if (rank == 0 and not a.no_telemetry) else None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    if tele is not None:
+        tele.start()
     t0 = time.perf_counter()
     for k in range(K):
         step(it, ev[k])
@@ -310,24 +429,19 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    telemetry = tele.stop() if tele is not None else None
     elapsed = t1 - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    kern_ms = float(np.mean([s_.elapsed_time(e) for s_, e in ev]))
     c1 = eng.read_counters()
     lf_local = int(c1[H.CNT_LEAPFROG] - c0[H.CNT_LEAPFROG])
     acc = int(c1[H.CNT_ACCEPT] - c0[H.CNT_ACCEPT])
-    if a.sampler == "nuts" and c1[H.CNT_ACCEPT] > 0:   # NUTS uses this slot for chain hand-off give-ups
-        raise RuntimeError("NUTS kernel: %d chain hand-offs timed out" % c1[H.CNT_ACCEPT])
+    if c1[H.CNT_HANDOFF_GIVEUP] > 0:
+        raise RuntimeError("NUTS kernel: %d chain hand-offs timed out" % c1[H.CNT_HANDOFF_GIVEUP])
     dmax_hits = int(c1[H.CNT_DMAX] - c0[H.CNT_DMAX])
     wave_steps = int(c1[H.CNT_LEAPFROG_SQ] - c0[H.CNT_LEAPFROG_SQ])   # NUTS: steps of 16-chain waves
-    tot = torch.tensor([float(lf_local), float(acc), float(dmax_hits), elapsed, kern_ms], dtype=torch.float64,
-                       device=dev)
-    if world > 1:
-        s = tot[:3].clone()
-        dist.all_reduce(s)
-        m = tot[3:].clone()
-        dist.all_reduce(m, op=dist.ReduceOp.MAX)
-        tot = torch.cat([s, m])
-    lf_all, acc_all, dmax_all, t_max, kern_max = tot.cpu().numpy().tolist()
+    lf_all, acc_all, dmax_all = reduce([float(lf_local), float(acc), float(dmax_hits)], dist.ReduceOp.SUM
+                                       if world > 1 else None)
+    t_max, kern_max = reduce([elapsed, kern_ms], dist.ReduceOp.MAX if world > 1 else None)
     value = lf_all / t_max
     ess = None
     if not a.no_ess:
@@ -344,13 +458,17 @@ def main():
         diag_s = time.perf_counter() - td
         ess = dict(ess_per_s_median=float(np.median(neff)) / t_samples,
                    ess_per_s_min=float(np.min(neff)) / t_samples,
+                   ess_per_s_median_incl_diag=float(np.median(neff)) / (t_samples + (0.0 if sd else diag_s)),
                    n_eff_median=float(np.median(neff)), n_eff_min=float(np.min(neff)),
                    rhat_median=float(np.median(R_hat)), rhat_max=float(np.max(R_hat)),
                    samples_per_chain=n_samples, sampling_s=t_samples, diagnostics_s=diag_s,
                    method=(f"streaming statistics (tmax={a.tmax}) over every timed sample, fed inside the timed loop"
                            if sd is not None else
                            f"reference estimator on the circular window's last {R} samples per chain (all chains), "
-                           f"after the timed loop; ESS/s = n_eff / time of the {R} iterations that produced them"))
+                           f"after the timed loop; ESS/s = n_eff / time of the {R} iterations that produced them "
+                           f"(ess_per_s_median_incl_diag adds the diagnostics' own time)"))
+    if world > 1:
+        dist.destroy_process_group()
 
     if rank == 0:
         dense = a.rho != 0 or nuts
@@ -367,23 +485,39 @@ def main():
         else:       # 8D per leapfrog + 8D energies per iteration
             flops_launch = lf_launch * 8 * D + N * S * 8 * D
         kern_s = kern_ms / 1e3
+        step_s = t_max / K
         tfl = flops_launch / kern_s / 1e12
         kname = "hmc_nuts_iters" if nuts else ("hmc_random_iters(dense)" if dense else "hmc_random_iters")
         shape = dict(kernel=kname, dim=D, chains_per_gpu=N, iters_per_step=S, window_rows=R,
                      stream_diag=bool(a.stream_diag), rho=a.rho)
         pm = pmc_traffic(shape)
+        traffic = None if pm is None else pm["bytes_per_launch"]
         hbm = {"bound": "hbm", "achieved": bytes_model / kern_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": bytes_model / kern_s / 1e9 / HBM_PEAK_GBS,
-               "traffic": None if pm is None else pm["bytes_per_launch"],
+               "traffic": traffic,
                "traffic_source": None if pm is None else pm.get("source"),
+               # measured HBM bytes (same-shape rocprofv3 PMC run) over the same kernel time: what
+               # the fused kernel actually moves, against the §8(d) model's unfused traffic above
+               "frac_measured": None if pm is None else traffic / kern_s / 1e9 / HBM_PEAK_GBS,
                "kernel": kname, "kernel_ms": kern_ms, "bytes_per_launch": bytes_model, "shape": shape,
                "bytes_model": "SURVEY.md §8(d): (24*D + 24) B per chain-iteration x chains x iterations per launch",
                "bytes_moved_per_launch": bytes_moved,
                "frac_moved": bytes_moved / kern_s / 1e9 / HBM_PEAK_GBS}
         mfma = {"bound": "mfma" if dense else "fp64 vector", "achieved": tfl, "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": tfl / FP64_PEAK_TFLOPS,
-                "traffic": None if pm is None else pm["bytes_per_launch"], "shape": shape, "kernel": kname,
+                "traffic": traffic, "shape": shape, "kernel": kname,
+                "hbm_frac_measured": None if pm is None else traffic / kern_s / 1e9 / HBM_PEAK_GBS,
                 "kernel_ms": kern_ms, "flops_per_launch": flops_launch}
+        if sd is not None:
+            # the timed step also feeds the streaming diagnostics: `frac` above prices the sampler
+            # launch alone (HIP events around it), frac_step the whole step `value` is timed on
+            for r_ in (hbm, mfma):
+                r_["step_ms"] = step_s * 1e3
+            hbm["frac_step"] = bytes_model / step_s / 1e9 / HBM_PEAK_GBS
+            mfma["frac_step"] = flops_launch / step_s / 1e12 / FP64_PEAK_TFLOPS
+        roof = mfma if dense else hbm
+        if telemetry is not None:
+            roof["telemetry"] = telemetry
         tdesc = f"rho={a.rho} dense-precision MVN" if a.rho != 0 else "unit MVN"
         samp = f"NUTS d_max={a.d_max} (overflow counted, not aborted)" if nuts else "Random-L HMC, L~U{5..19}"
         store_desc = (f"every q_chain row, E, dE stored (circular window of {R} rows)" if store else
@@ -395,31 +529,32 @@ def main():
             "n_gpus": world,
             "steps": K,
             "warmup": W,
-            "ms_per_step": t_max / K * 1e3,
+            "ms_per_step": step_s * 1e3,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak" if weak else "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": f"synthetic (D={D} {tdesc}, starts ~ N(0, 2I), Philox4x32-10 draws)",
-            "config": {"workload": f"{samp}, D={D} {tdesc}, dt={a.dt}, {a.chains} chains in total "
+            "data": f"synthetic (D={D} {tdesc}, starts ~ N(0, 2I) keyed by global chain id, Philox4x32-10 draws)",
+            "config": {"workload": f"{samp}, D={D} {tdesc}, dt={a.dt}, {chains_total} chains in total "
                                    f"({N} on rank 0), {S} iterations per step (one fused launch), "
                                    f"{store_desc}, fp_mode={a.fp_mode}",
-                       "chains_total": a.chains, "chains_per_gpu": N, "dim": D, "iters_per_step": S,
-                       "window_rows": R, "parallelism": f"chains{world}"},
-            "roofline": mfma if dense else hbm,
+                       "preset": a.config, "chains_total": chains_total, "chains_per_gpu": N, "dim": D,
+                       "iters_per_step": S, "window_rows": R, "parallelism": f"chains{world}",
+                       "backend": a.backend if world > 1 else None},
+            "roofline": roof,
             "compute" if not dense else "memory": mfma if not dense else hbm,
-            "accept_rate": None if nuts else acc_all / (a.chains * K * S),
-            "leapfrog_per_iteration": lf_all / (a.chains * K * S),
+            "leapfrogs": int(lf_all),
+            "accepts": None if nuts else int(acc_all),
+            "accept_rate": None if nuts else acc_all / (chains_total * K * S),
+            "leapfrog_per_iteration": lf_all / (chains_total * K * S),
             "lane_utilisation": (lf_local / (16.0 * wave_steps)) if nuts and wave_steps else None,
-            "dmax_fraction": (dmax_all / (a.chains * K * S)) if nuts else None,
+            "dmax_fraction": (dmax_all / (chains_total * K * S)) if nuts else None,
             "debug_env_unset": True,
             "ess": ess,
         }
-        if world == 1 and not a.no_cpu_baseline:
+        if not a.no_cpu_baseline:       # rank 0 at any N, after every rank left the timed region
             line["cpu_baseline"] = cpu_baseline(D, a.cpu_seconds, a.rho, a.sampler, a.d_max)
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

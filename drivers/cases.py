@@ -8,10 +8,12 @@ Each reference script runs one target family at D = 2, 10, 100 (variants a, b, c
 with Niter 2000, 10 chains, warm-up 1000, thin 1, dt 0.1, L ~ U{5..19}, 100 saved chain-0
 trajectories, starts ~ N(q0, 2I) (x100 for case 2).  The driver builds the same V/dVdq
 closures and calls the same HMC_sampler surface; the sampler probes the closures into an MVN
-descriptor and runs the fused HIP kernels.  plot_samples/make_movie are host matplotlib
-outside the accelerated path and are skipped.
+descriptor and runs the fused HIP kernels.  Like every reference script, a run ends with
+plot_samples (savefig, the 3x3 summary PNG) and make_movie (the chain-0 PNG deck) on the
+GPU-filled sampler (case1-script.py:66-67), written under --out-dir as the reference's
+./caseN/caseNx prefixes; --no-plots skips them, --movie-frames caps the deck.
 
-    python drivers/cases.py 1a [--seed 0] [--chains N --rng philox] [--sampler NUTS]
+    python drivers/cases.py 1a [--seed 0] [--chains N --rng philox] [--sampler NUTS] [--no-plots]
 """
 import argparse
 import os
@@ -46,9 +48,18 @@ def target(D, rho):
     return q0, cov0, V, dVdq
 
 
+def title_prefix(name, out_dir="."):
+    """The reference's title_str: ./case1/case1a ... (case3-script-2.py: ./case3/case3d)."""
+    fam = name.split("-")[0][0]
+    tag = "3d" if name == "3-2" else name
+    return os.path.join(out_dir, "case%s" % fam, "case%s" % tag)
+
+
 def run_case(name, seed=None, chains=None, rng="replay", sampler="Random", d_max=10, verbose=True,
-             fp_mode="exact"):
-    """Run one case; returns the HMC_sampler (reference attributes filled)."""
+             fp_mode="exact", plots=False, out_dir=".", movie_frames=None, movie_dpi=200):
+    """Run one case; returns the HMC_sampler (reference attributes filled).  plots=True ends the
+    run as the reference scripts do (case1-script.py:66-67): plot_samples(savefig) and make_movie
+    into title_prefix(name, out_dir); h.plot_summary / h.movie_files hold what they drew."""
     from hmc_amd.samplers import HMC_sampler
     from hmc_amd.utils import start_pts
     c = dict(CASES[name])
@@ -85,7 +96,18 @@ def run_case(name, seed=None, chains=None, rng="replay", sampler="Random", d_max
         print("R-hat: ", h.R_q)
         print("leapfrog steps: %d in %.3f s (%.3e /s incl. host streams and copies)"
               % (h.n_leapfrog, wall, h.n_leapfrog / wall))
-        print("(plot_samples / make_movie: host matplotlib, skipped)\n")
+    h.plot_summary, h.movie_files = None, None
+    if plots:
+        title = title_prefix(name, out_dir)
+        os.makedirs(os.path.dirname(title), exist_ok=True)
+        h.plot_summary = h.plot_samples(title_prefix=title, savefig=True, show=False, plot_normal=True, q0=q0,
+                                        cov0=cov0)
+        if sampler == "Random":                          # the reference's movie is Random-only (:850)
+            lim = 1100 if c["far_chain0"] else 4         # case2-script.py:69 / case1-script.py:67
+            h.movie_files = h.make_movie(title_prefix=title, q0=q0, cov0=cov0, plot_cov=True, qmin=-lim, qmax=lim,
+                                         max_frames=movie_frames, dpi=movie_dpi)
+    if verbose:
+        print()
     return h
 
 
@@ -98,9 +120,13 @@ def main():
     ap.add_argument("--sampler", default="Random", choices=["Random", "NUTS"])
     ap.add_argument("--d-max", type=int, default=10)
     ap.add_argument("--fp-mode", default="exact", choices=["exact", "fast"])
+    ap.add_argument("--no-plots", action="store_true", help="skip plot_samples / make_movie")
+    ap.add_argument("--out-dir", default=".", help="where the ./caseN/caseNx figure prefixes go")
+    ap.add_argument("--movie-frames", type=int, default=None, help="cap on make_movie slides (default: all)")
     a = ap.parse_args()
     for name in a.case:
-        run_case(name, seed=a.seed, chains=a.chains, rng=a.rng, sampler=a.sampler, d_max=a.d_max, fp_mode=a.fp_mode)
+        run_case(name, seed=a.seed, chains=a.chains, rng=a.rng, sampler=a.sampler, d_max=a.d_max, fp_mode=a.fp_mode,
+                 plots=not a.no_plots, out_dir=a.out_dir, movie_frames=a.movie_frames)
 
 
 if __name__ == "__main__":

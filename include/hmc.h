@@ -44,8 +44,7 @@ enum { HMC_MODE_EXACT = 0, HMC_MODE_FAST = 1 };
 
 /* counters[] slots (unsigned long long, device, accumulated with atomics) */
 enum {
-  HMC_CNT_ACCEPT = 0,        /* accepted proposals, i >= warm_up (samplers.py:467); NUTS:
-                                chain hand-offs between slots given up (a launch error, 0)   */
+  HMC_CNT_ACCEPT = 0,        /* accepted proposals, i >= warm_up (samplers.py:467)          */
   HMC_CNT_ACCEPT_WU = 1,     /* accepted proposals, i <  warm_up (samplers.py:469)          */
   HMC_CNT_LEAPFROG = 2,      /* sum of L actually integrated (the metric's unit of work)     */
   HMC_CNT_LEAPFROG_SQ = 3,   /* Random: sum of L^2 (N_total_steps, Q13); NUTS: wave steps    */
@@ -53,7 +52,9 @@ enum {
   HMC_CNT_UNSTABLE = 5,      /* NUTS |E-E0| > 1000 sub-tree rejections (samplers.py:647)     */
   HMC_CNT_DMAX = 6,          /* NUTS chain-iterations that hit d_max                         */
   HMC_CNT_ENERGY_EVALS = 7,  /* NUTS energy evaluations (N_total_steps accounting)           */
-  HMC_NCOUNTERS = 8,
+  HMC_CNT_HANDOFF_GIVEUP = 8,/* NUTS chain hand-offs between work-queue slots given up (a
+                                launch error: must stay 0; the Python layer raises)           */
+  HMC_NCOUNTERS = 9,
   /* counters are spread over HMC_COUNTER_SLOTS rows ([slot][HMC_NCOUNTERS]) so that the
    * per-wave atomics of a launch do not serialise on one address; totals = sum over slots */
   HMC_COUNTER_SLOTS = 4096
@@ -231,6 +232,20 @@ int64_t hmc_variogram_work_size(int64_t n_chains, int32_t D, int32_t nlags);
 hmc_status hmc_variogram(const double* x, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
                          int64_t base, int32_t n, int32_t D, int32_t t0, int32_t t1, double* work, double* out,
                          void* stream);
+
+/* Everything convergence_stats needs from the samples in ONE pass (utils.py:88-126, :161-179):
+ * out[(3 + tmax)][D] =
+ *   row 0        sum_j std_j (ddof=1)                       (W, utils.py:109-112)
+ *   row 1        sum_j (mean_j - S_d)                       (mean_all, :116-119)
+ *   row 2        sum_j (mean_j - S_d)^2                     (B, :120, after re-centring)
+ *   row 2 + t    sum_j sum_s (x_j[s+t] - x_j[s])^2, t = 1..tmax (variogram, :161-179; valid for t < n)
+ * over the 2*n_chains split chains j (same strided view as hmc_split_moments), S_d = x[base + d]
+ * (the view's first sample: a common shift so that B needs no second pass).  tmax in {8, 16, 32};
+ * longer lags: hmc_variogram.  Deterministic (fixed-order two-stage sums). */
+int64_t hmc_convergence_work_size(int64_t n_chains, int32_t D, int32_t tmax);
+hmc_status hmc_convergence_sums(const double* x, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
+                                int64_t base, int32_t n, int32_t D, int32_t tmax, double* work, double* out,
+                                void* stream);
 
 /* Streaming (windowed) split-chain statistics for runs whose q_chain does not fit: feed the
  * samples segment by segment.  Positions p index q_chain[:, 1:, :] (Q16); p lies in split half

@@ -14,7 +14,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG_DIR = os.path.join(ROOT, "understanding-hmc_amd")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
-for p in (ROOT, PKG_DIR):
+for p in (ROOT, PKG_DIR, os.path.join(ROOT, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 

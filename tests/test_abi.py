@@ -41,6 +41,20 @@ def test_struct_layouts():
     assert ctypes.sizeof(H.State) == 9 * 8 + 8 + 2 * 8 + 8
 
 
+def test_counter_slots_match_header():
+    """Every HMC_CNT_* slot of include/hmc.h has its mirror in _lib (one meaning per slot: the NUTS
+    hand-off give-ups have their own slot, HMC_CNT_HANDOFF_GIVEUP, not HMC_CNT_ACCEPT's)."""
+    from hmc_amd import _lib as H
+    src = open(os.path.join(ROOT, "include", "hmc.h")).read()
+    slots = {k: int(v) for k, v in re.findall(r"HMC_CNT_(\w+)\s*=\s*(\d+)", src)}
+    assert slots, "no counter slots found"
+    for k, v in slots.items():
+        assert getattr(H, "CNT_" + k) == v, k
+    assert sorted(slots.values()) == list(range(len(slots)))
+    assert int(re.search(r"HMC_NCOUNTERS\s*=\s*(\d+)", src).group(1)) == H.NCOUNTERS == len(slots)
+    assert int(re.search(r"HMC_COUNTER_SLOTS\s*=\s*(\d+)", src).group(1)) == H.COUNTER_SLOTS
+
+
 def test_invalid_arguments_map_to_reference_exceptions():
     """Validation runs on the host before any HIP call: the reference's asserts become
     AssertionError via hmc_status HMC_EINVAL (samplers.py:331-348)."""

@@ -62,3 +62,33 @@ def test_debug_env_refused():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run"], capture_output=True,
                          text=True, env=env, timeout=120)
     assert out.returncode != 0 and "HMC_DEBUG_ABLATE" in out.stderr
+
+
+def test_presets_resolve_baseline_configs():
+    """--config picks the BASELINE.json shapes; explicit flags still override the preset."""
+    a = bench.parse(["--config", "c3"])
+    assert (a.chains, a.dim, a.rho, a.sampler) == (262144, 100, 0.95, "random")
+    a = bench.parse(["--config", "c5", "--steps", "7"])
+    assert (a.chains, a.rho, a.sampler, a.steps, a.warmup) == (65536, 0.95, "nuts", 7, 1)
+    a = bench.parse(["--config", "c4"])
+    assert a.stream_diag and a.dim == 1000
+    assert bench.resolve_chains(a, 8) == (1048576, True)      # c4: 1,048,576 chains on 8 GPUs
+    assert bench.resolve_chains(a, 1) == (131072, True)
+    a = bench.parse([])
+    assert bench.resolve_chains(a, 8) == (1048576, False)     # the metric: 1M chains at any N
+    a = bench.parse(["--config", "c1"])
+    assert (a.chains, a.dim, a.iters_per_step * a.warmup, a.iters_per_step * a.steps) == (10, 2, 1000, 1000)
+
+
+def test_c4_dry_run_prints_eight_shards():
+    """The c4 job as 8 ranks: 131,072 chains x D=1000 each, 1,048,576 in total."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "c4", "--gpus", "8",
+                          "--dry-run"], capture_output=True, text=True, env=env, timeout=400)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rep = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert rep["n_gpus"] == 8 and rep["chains_total"] == 1048576 and rep["scaling"] == "weak"
+    assert rep["dim"] == 1000
+    shards = sorted(rep["shards"])
+    assert [s[1] for s in shards] == [131072 * r for r in range(8)]
+    assert all(s[2] == 131072 for s in shards)

@@ -1,16 +1,16 @@
 """The production (Philox) kernel instantiations pinned to the oracle.
 
-bench.py times `k_wave_iters_k1<EXACT=false, GEN=false, REPLAY=false, FULL=false>` (in-kernel
-Philox4x32-10 draws, FAST integrator, no capture hooks), the dense L-ordered-tile kernel and the
-NUTS kernel in Philox mode.  Here every random number those kernels consume is regenerated on
-the host from the same counters and replayed through the oracle (oracle/hmc_oracle.py, which
-restates samplers.py:387-491 / :495-808):
-  * momentum: the table-driven Box-Muller normals the kernels draw, read back through the C-ABI
-    debug entry hmc_rng_normals (same transform, same (slot, iteration, global chain) counter);
-    the initial momentum (iteration 0, samplers.py:415) uses the libm-free Box-Muller of
-    hmc_device.hpp::normal_pair, restated here with NumPy (agrees to ~4e-15 of the radius,
-    test_gpu_random.py::test_philox_normals_match_numpy_box_muller); the NUTS momenta use the
-    table transform too;
+bench.py times `k_wave_iters_k1<EXACT=false, GEN=false, REPLAY=false, FULL=false>` (D <= 128:
+in-kernel Philox4x32-10 draws through the momentum ring, FAST integrator, no capture hooks),
+`k_wave_iters<K=2/4/8, ..., FULL=false>` (D > 128, BASELINE config 4: per-lane momentum draws,
+streaming window), the dense L-ordered-tile kernel and the NUTS kernel in Philox mode.  Here every
+random number those kernels consume is regenerated on the HOST from the same counters
+(tests/philox_host.py: NumPy Philox4x32-10 and the table-driven Box-Muller restated) and replayed
+through the oracle (oracle/hmc_oracle.py, which restates samplers.py:387-491 / :495-808):
+  * momentum of iteration >= 1: the table Box-Muller (hmc_device.hpp::normal_pair_tab) restated in
+    NumPy; the initial momentum (iteration 0, samplers.py:415) plain Box-Muller
+    (hmc_device.hpp::normal_pair); test_table_normals_match_kernel pins the restatement to the
+    kernels' generator (C-ABI debug entry hmc_rng_normals) to 1e-13;
   * trajectory length L (samplers.py:441) and MH log-uniform (:461): Philox block
     (0x80000000, iteration, chain lo, chain hi): L = L_low + (x * (L_high - L_low)) >> 32,
     u = ((w << 21) | (z >> 11)) * 2^-53, log u (NumPy log; the kernel's fast_log is within 1 ulp);
@@ -24,58 +24,9 @@ import pytest
 import torch
 
 from oracle import hmc_oracle as O
+from philox_host import KDRAW, bm_pair, host_L_lnu, table_normals, u53, wave_momenta, words
 
 pytestmark = pytest.mark.gpu
-
-KDRAW = 0x80000000
-M32 = np.uint64(0xFFFFFFFF)
-
-
-def np_philox(ctr, key):
-    """Vectorised Philox4x32-10: ctr (n, 4) words, key (k0, k1) -> 4 uint64 arrays."""
-    c = [ctr[:, i].astype(np.uint64) for i in range(4)]
-    k0, k1 = np.uint64(key[0]), np.uint64(key[1])
-    for _ in range(10):
-        p0 = c[0] * np.uint64(0xD2511F53)
-        p1 = c[2] * np.uint64(0xCD9E8D57)
-        c = [((p1 >> np.uint64(32)) ^ c[1] ^ k0) & M32, p1 & M32, ((p0 >> np.uint64(32)) ^ c[3] ^ k1) & M32, p0 & M32]
-        k0 = (k0 + np.uint64(0x9E3779B9)) & M32
-        k1 = (k1 + np.uint64(0xBB67AE85)) & M32
-    return c
-
-
-def words(slot, it, gc, seed):
-    """Philox blocks for counters (slot, it, gc): broadcast over array arguments."""
-    slot, it, gc = np.broadcast_arrays(np.asarray(slot, np.uint64), np.asarray(it, np.uint64),
-                                       np.asarray(gc, np.uint64))
-    shape = slot.shape
-    ctr = np.stack([slot.ravel(), it.ravel(), gc.ravel() & M32, gc.ravel() >> np.uint64(32)], axis=1)
-    w = np_philox(ctr, (seed & 0xFFFFFFFF, seed >> 32))
-    return [x.reshape(shape) for x in w]
-
-
-def bm_pair(w):
-    """hmc_device.hpp::normal_pair restated: Box-Muller on 52-bit uniforms."""
-    a = ((w[1] << np.uint64(20)) | (w[0] >> np.uint64(12))).astype(np.float64)
-    b = ((w[3] << np.uint64(20)) | (w[2] >> np.uint64(12))).astype(np.float64)
-    r = np.sqrt(-2.0 * np.log(1.0 - a * 2.0 ** -52))
-    ang = 2 * np.pi * (b * 2.0 ** -52)
-    return r * np.cos(ang), r * np.sin(ang)
-
-
-def u53(z, w):
-    return ((w << np.uint64(21)) | (z >> np.uint64(11))).astype(np.float64) * 2.0 ** -53
-
-
-def host_L_lnu(seed, gcs, niter, lo, hi):
-    """(N, Niter) trajectory lengths and log-uniforms of iterations 1..Niter."""
-    it = np.arange(1, niter + 1)[None, :]
-    w = words(KDRAW, it, gcs[:, None], seed)
-    L = lo + ((w[0] * np.uint64(hi - lo)) >> np.uint64(32)).astype(np.int64)
-    u = u53(w[2], w[3])
-    with np.errstate(divide="ignore"):
-        lnu = np.log(u)
-    return L.astype(np.int32), lnu
 
 
 def gpu_normals(seed, chain0, n, it, npairs):
@@ -86,15 +37,15 @@ def gpu_normals(seed, chain0, n, it, npairs):
     return out.cpu().numpy()
 
 
-def wave_momenta(seed, N, D, niter):
-    """Diagonal kernels: pair k holds dims 2k, 2k+1 (slot k).  p0 (iteration 0) from normal_pair,
-    iterations >= 1 from the table transform."""
-    npairs = (D + 1) // 2
-    gcs = np.arange(N, dtype=np.uint64)
-    z0, z1 = bm_pair(words(np.arange(npairs)[None, :], 0, gcs[:, None], seed))
-    p0 = np.stack([z0, z1], axis=2).reshape(N, 2 * npairs)[:, :D]
-    P = np.stack([gpu_normals(seed, 0, N, it, npairs)[:, :D] for it in range(1, niter + 1)], axis=1)
-    return p0, P
+@pytest.mark.parametrize("npairs,chain0,it", [(50, 0, 1), (500, 1 << 33, 17), (64, 12345, 999)])
+def test_table_normals_match_kernel(npairs, chain0, it):
+    """The host restatement of the table Box-Muller equals the kernels' generator to 1e-13
+    (both are ~1-ulp evaluations of the same function of the same Philox words)."""
+    seed = 0x1234_5678_9ABC
+    g = gpu_normals(seed, chain0, 96, it, npairs)
+    h = table_normals(seed, chain0, 96, it, npairs)
+    assert np.all(np.isfinite(g))
+    np.testing.assert_allclose(g, h, rtol=0, atol=1e-13)
 
 
 def dense_slot_index(D):
@@ -113,7 +64,7 @@ def dense_momenta(seed, N, D, niter, table=True):
     P = np.empty((N, niter, D))
     for it in range(1, niter + 1):
         if table:
-            g = gpu_normals(seed, 0, N, it, D)
+            g = table_normals(seed, 0, N, it, D)
             P[:, it - 1] = g[:, 2 * slot + which]
         else:
             z = bm_pair(words(slot[None, :], it, gcs[:, None], seed))
@@ -148,7 +99,10 @@ def test_wave_production_kernel_vs_oracle(fp_mode):
                     warm_up_num=wu, target=MVNTarget(np.zeros(D), np.eye(D)), rng="philox", seed=seed,
                     fp_mode=fp_mode)
     h.gen_sample(q_start, verbose=False)
-    p0, P = wave_momenta(seed, N, D, Niter)
+    # EXACT asserts the integrator bit for bit, so it replays the generator's own output (read back
+    # through hmc_rng_normals, itself pinned to the host restatement by test_table_normals_match_kernel);
+    # FAST replays the host restatement
+    p0, P = wave_momenta(seed, N, D, Niter, normals=gpu_normals if fp_mode == "exact" else table_normals)
     L, lnu = host_L_lnu(seed, np.arange(N, dtype=np.uint64), Niter, 5, 20)
     ref = O.gen_sample_random(O.HMCCore(O.MVNTarget(np.zeros(D), np.eye(D)), 0.1), q_start, N, Niter, wu, 1, 5, 20,
                               O.ReplayDraws(p0, P, L, lnu))
@@ -191,6 +145,110 @@ def test_wave_production_window_vs_oracle():
     c = eng.read_counters()
     from hmc_amd import _lib as H
     assert int(c[H.CNT_LEAPFROG]) == ref["n_leapfrog"]
+
+
+class UnitCore(O.HMCCore):
+    """oracle HMCCore for an identity precision and mass: np.dot(I, g) == g exactly, so the
+    half kicks are written without the D x D products (same arithmetic, D=1000 stays fast)."""
+
+    def leap_frog(self, p_old, q_old):              # samplers.py:831-839 with inv_cov_p = inv_cov0 = I
+        p_half = p_old - self.dt * (q_old - self.t.q0) / 2.
+        q_new = q_old + self.dt * p_half
+        p_new = p_half - self.dt * (q_new - self.t.q0) / 2.
+        return p_new, q_new
+
+
+class UnitMVN(FastMVN):
+    def __init__(self, D):
+        self.q0 = np.zeros(D)
+        self.c = D * np.log(2 * np.pi)
+
+    def V(self, q):
+        x = q - self.q0
+        return 0.5 * (self.c + x @ x)
+
+
+@pytest.mark.parametrize("D", [129, 200, 300, 1000])
+def test_wave_kgt1_production_streaming_vs_oracle(D):
+    """BASELINE config 4's benchmarked instance, k_wave_iters<K = 2, 2, 4, 8, FAST, Philox,
+    FULL=false> (per-lane wave_momentum draws, D > 128; odd D = 129 included), driven the way
+    bench.py --stream-diag drives it: RandomEngine.run_streaming (circular q_chain window, several
+    fused launches, the streaming statistics fed every `feed` iterations, tmax = 16).  The oracle
+    replays the host-regenerated draws: accept and leapfrog counts exact, q and E_chain to
+    1e-9 / 1e-10, streamed R-hat equal to the oracle's convergence_stats (utils.py:77-126) to
+    1e-10 and ESS wherever the reference reads no lag beyond tmax."""
+    from hmc_amd import _lib as H
+    from hmc_amd.diagnostics import StreamingDiagnostics
+    from hmc_amd.engine import RandomEngine
+    from hmc_amd.target import MVNTarget
+    N, Niter, wu, seed, step, feed = 48, 24, 3, 0xC4_0000 + D, 4, 8
+    eng = RandomEngine(MVNTarget(np.zeros(D), np.eye(D)), N, Niter, wu, 1, 5, 20, 0.1, rng="philox", seed=seed,
+                       fp_mode="fast", store_chain=False)
+    q_start = np.random.RandomState(D).standard_normal((N, D)) * np.sqrt(2.0)
+    eng.init(q_start)
+    sd = StreamingDiagnostics(N, D, eng.L_chain - 1, tmax=16)
+    eng.run_streaming(sd, 1, Niter + 1, step, feed=feed)
+    R, neff = sd.finish()
+    p0, P = wave_momenta(seed, N, D, Niter)
+    L, lnu = host_L_lnu(seed, np.arange(N, dtype=np.uint64), Niter, 5, 20)
+    ref = O.gen_sample_random(UnitCore(UnitMVN(D), 0.1), q_start, N, Niter, wu, 1, 5, 20,
+                              O.ReplayDraws(p0, P, L, lnu))
+    c = eng.read_counters()
+    assert int(c[H.CNT_ACCEPT]) == ref["accept_count"] and int(c[H.CNT_ACCEPT_WU]) == ref["accept_count_warm_up"]
+    assert int(c[H.CNT_LEAPFROG]) == ref["n_leapfrog"] == int(L.sum())
+    np.testing.assert_allclose(eng.q.cpu().numpy(), ref["q_chain"][:, -1], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(eng.E_chain.cpu().numpy(), ref["E_chain"], rtol=1e-10)
+    R_ref, neff_ref = O.convergence_stats(ref["q_chain"][:, 1:, :], thin_rate=1, warm_up_num=0)
+    np.testing.assert_allclose(R, R_ref, rtol=1e-10)
+    from test_gpu_stream import _lags_needed
+    ok = _lags_needed(ref["q_chain"][:, 1:, :]) <= 16
+    assert ok.sum() >= 5
+    np.testing.assert_allclose(neff[ok], neff_ref[ok], rtol=1e-10)
+
+
+def test_wave_c4_shard_full_shape():
+    """One config-4 shard at its benchmarked size: 131,072 chains x D = 1000 (K = 8), Philox,
+    streaming window and statistics, started in the stationary law N(0, I).  Acceptance near the
+    c4 bench's 0.973, leapfrogs per iteration 12, the law preserved, and the two halves run as
+    separate shards (chain_offset) bit-identical to the whole, streamed sums included."""
+    from hmc_amd import _lib as H
+    from hmc_amd.diagnostics import StreamingDiagnostics
+    from hmc_amd.engine import RandomEngine
+    from hmc_amd.target import MVNTarget
+    N, D, Niter, wu, step = 131072, 1000, 30, 1, 10
+    g = torch.Generator(device="cuda").manual_seed(44)
+    qs = torch.randn((N, D), dtype=torch.float64, device="cuda", generator=g)
+
+    def run(lo, hi):
+        eng = RandomEngine(MVNTarget(np.zeros(D), np.eye(D)), hi - lo, Niter, wu, 1, 5, 20, 0.1, rng="philox",
+                           seed=0xC4, fp_mode="fast", chain_offset=lo, store_chain=False)
+        eng.init(qs[lo:hi].contiguous())
+        sd = StreamingDiagnostics(hi - lo, D, eng.L_chain - 1, tmax=16)
+        eng.run_streaming(sd, 1, Niter + 1, step, feed=step)
+        torch.cuda.synchronize()
+        out = (eng.q.clone(), eng.read_counters(), sd)
+        del eng
+        return out
+
+    q_all, c_all, sd_all = run(0, N)
+    acc = c_all[H.CNT_ACCEPT] / (N * Niter)
+    assert abs(acc - 0.973) < 0.01, acc
+    assert abs(c_all[H.CNT_LEAPFROG] / (N * Niter) - 12.0) < 0.02
+    x = q_all.cpu().numpy()
+    assert np.abs(x.mean(axis=0)).max() < 6 / np.sqrt(N)
+    assert np.abs(x.var(axis=0) - 1).max() < 6 * np.sqrt(2 / N)
+    R, neff = sd_all.finish()
+    assert np.all(np.isfinite(R)) and np.all(np.abs(R - 1) < 0.01)
+    assert np.all(neff > 0)
+    cut = N // 2 + 40
+    qa, ca, sa = run(0, cut)
+    qb, cb, sb = run(cut, N)
+    assert torch.equal(torch.cat([qa, qb]), q_all)
+    assert ca[H.CNT_LEAPFROG] + cb[H.CNT_LEAPFROG] == c_all[H.CNT_LEAPFROG]
+    assert ca[H.CNT_ACCEPT] + cb[H.CNT_ACCEPT] == c_all[H.CNT_ACCEPT]
+    for k in ("shift", "s1", "s2"):
+        assert torch.equal(torch.cat([getattr(sa, k), getattr(sb, k)]), getattr(sd_all, k))
+    torch.testing.assert_close(sa.vsum + sb.vsum, sd_all.vsum, rtol=1e-12, atol=0)
 
 
 @pytest.mark.parametrize("fp_mode", ["fast", "exact"])

@@ -168,6 +168,110 @@ __global__ __launch_bounds__(256) void k_variogram_ring(Src s, int t0, int nt, i
   }
 }
 
+// ---- ONE pass for convergence_stats (utils.py:88-126 and :161-179).  Per split chain j (n samples)
+// and dim d, with y = x - x_j[0] (shifted: the sums stay well conditioned):
+//   s1 = sum y, s2 = sum y^2  ->  mean_j = x_j[0] + s1/n, std_j = sqrt((s2 - s1 s1/n)/(n - 1))
+//   V_t,j = sum_{s<n-t} (y[s+t] - y[s])^2 = 2 s2 - P_t - Q_t - 2 C_t,  C_t = sum_s y[s] y[s+t],
+//   P_t = sum_{s<t} y^2 (the first t samples), Q_t = sum_{s>=n-t} y^2 (the last t)
+// so a lag costs ONE FMA per sample (v[t] += (-2 y[s]) y[s-t-1] against a register ring of the last
+// T samples) instead of a subtraction and an FMA.  Sums over the block's split chains:
+//   row 0: sum_j std_j, row 1: sum_j (mean_j - S_d), row 2: sum_j (mean_j - S_d)^2,
+//   row 3 + t - 1: sum_j V_t,j for lags t = 1..T (valid for t < n), S_d = x[base + d].
+// Block = 4 split-chain rows x 64 dims (lane = dim: coalesced rows).  The dim tiles of one chain
+// group run on the same XCD (block b on XCD b % 8), so a row's line shared by two tiles is fetched
+// from HBM once.
+constexpr int kConvUnroll = 8;
+
+template <int T>
+__global__ __launch_bounds__(256) void k_conv_fused(Src s, int groups, int ntiles, double* partial) {
+  __shared__ double red[4][kDimTile];
+  const int dl = threadIdx.x & (kDimTile - 1);
+  const int rl = threadIdx.x / kDimTile;
+  const int b = blockIdx.x;                       // XCD-aware: tiles of a group 8 blocks apart
+  const int tile = (b >> 3) % ntiles;
+  const int grp = (b & 7) + 8 * ((b >> 3) / ntiles);
+  const int d = tile * kDimTile + dl;
+  const int64_t m2 = 2 * s.n_chains;
+  const int64_t ss = s.sample_stride;
+  const int n = s.n;
+  double v[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) v[t] = 0.0;
+  double a_std = 0.0, a_m = 0.0, a_m2 = 0.0;
+  if (d < s.D && grp < groups) {
+    const double S = s.x[s.base + d];
+    for (int64_t j = (int64_t)grp * 4 + rl; j < m2; j += (int64_t)groups * 4) {
+      const double* bp = split_ptr(s, j, 0) + d;
+      const double sh = bp[0];
+      double ring[T];
+#pragma unroll
+      for (int k = 0; k < T; ++k) ring[k] = 0.0;
+      double s1 = 0.0, s2 = 0.0;
+      // first T samples: their running sum of squares gives P_t (lag t = i + 1)
+#pragma unroll
+      for (int i = 0; i < T; ++i) {
+        if (i < n) {
+          const double y = bp[(int64_t)i * ss] - sh;
+          s1 += y;
+          s2 = __builtin_fma(y, y, s2);
+          const double ym2 = -2.0 * y;
+#pragma unroll
+          for (int t = 0; t < i; ++t) v[t] = __builtin_fma(ym2, ring[t], v[t]);
+          v[i] -= s2;
+#pragma unroll
+          for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
+          ring[0] = y;
+        }
+      }
+      for (int i0 = T; i0 < n; i0 += kConvUnroll) {
+        double xs[kConvUnroll];
+#pragma unroll
+        for (int u = 0; u < kConvUnroll; ++u) xs[u] = (i0 + u < n) ? bp[(int64_t)(i0 + u) * ss] : 0.0;
+#pragma unroll
+        for (int u = 0; u < kConvUnroll; ++u) {
+          if (i0 + u < n) {                       // uniform
+            const double y = xs[u] - sh;
+            s1 += y;
+            s2 = __builtin_fma(y, y, s2);
+            const double ym2 = -2.0 * y;
+#pragma unroll
+            for (int t = 0; t < T; ++t) v[t] = __builtin_fma(ym2, ring[t], v[t]);
+#pragma unroll
+            for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
+            ring[0] = y;
+          }
+        }
+      }
+      // the last T samples (ring[k] = y[n-1-k]) give Q_t; every lag gets 2 s2
+      double q = 0.0;
+      const double s2x2 = 2.0 * s2;
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        q = __builtin_fma(ring[t], ring[t], q);
+        v[t] += s2x2 - q;
+      }
+      const double mu = s1 / n;
+      const double var = (s2 - s1 * mu) / (n - 1);
+      a_std += sqrt(var > 0.0 ? var : 0.0);
+      const double e = (sh - S) + mu;
+      a_m += e;
+      a_m2 = __builtin_fma(e, e, a_m2);
+    }
+  }
+  auto put = [&](int row, double x) {
+    red[rl][dl] = x;
+    __syncthreads();
+    if (rl == 0 && d < s.D && grp < groups)
+      partial[((int64_t)grp * (T + 3) + row) * s.D + d] = ((red[0][dl] + red[1][dl]) + red[2][dl]) + red[3][dl];
+    __syncthreads();
+  };
+  put(0, a_std);
+  put(1, a_m);
+  put(2, a_m2);
+#pragma unroll
+  for (int t = 0; t < T; ++t) put(3 + t, v[t]);
+}
+
 // ---- streaming (windowed) split-chain statistics: q_chain never has to be stored whole.
 // Sample position p (0-based over q_chain[:, 1:, :]) lies in split half h = p / n at offset
 // s = p - h*n (positions >= 2n are not part of any split chain, utils.py:102-104).  A call
@@ -286,6 +390,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T <= 16 ? 3
 
 int64_t rows_chunks(int64_t rows) { return (rows + kRowChunk - 1) / kRowChunk; }
 
+int64_t conv_groups(int64_t n_chains) {
+  const int64_t g = (2 * n_chains + 3) / 4;       // 4 split chains per block row set
+  const int64_t cap = 512;                        // ~2 resident blocks per CU per dim tile
+  return g < cap ? (g < 1 ? 1 : g) : cap;
+}
+
 int64_t vario_jchunk(int64_t m2) {
   // ~4096 blocks at most; at least 16 split chains per block
   int64_t c = (m2 + 4095) / 4096;
@@ -319,6 +429,28 @@ hipError_t launch_rowsum(const double* x, int64_t n_outer, int64_t os, int64_t n
   k_rowsum_partial<<<grid, 256, 0, st>>>(r, work);
   if (hipError_t e = hipGetLastError()) return e;
   k_colsum_final<<<(unsigned)((D + 255) / 256), 256, 0, st>>>(work, nch, D, out);
+  return hipGetLastError();
+}
+
+int64_t diag_conv_work(int64_t n_chains, int D, int T) { return conv_groups(n_chains) * (int64_t)(T + 3) * D; }
+
+hipError_t launch_conv_fused(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int64_t base, int n, int D,
+                             int T, double* work, double* out, hipStream_t st) {
+  Src s{x, cs, ss, base, n_chains, n, D};
+  const int64_t groups = conv_groups(n_chains);
+  const int ntiles = (D + kDimTile - 1) / kDimTile;
+  // blocks: 8 groups x ntiles per 8 * ntiles consecutive block ids (XCD-aware order, see kernel)
+  const int64_t gpad = (groups + 7) / 8 * 8;
+  const dim3 grid((unsigned)(gpad * ntiles));
+  switch (T) {
+    case 8: k_conv_fused<8><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
+    case 16: k_conv_fused<16><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
+    case 32: k_conv_fused<32><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
+    default: return hipErrorInvalidValue;
+  }
+  if (hipError_t e = hipGetLastError()) return e;
+  const int64_t ncols = (int64_t)(T + 3) * D;
+  k_colsum_final<<<(unsigned)((ncols + 255) / 256), 256, 0, st>>>(work, groups, ncols, out);
   return hipGetLastError();
 }
 

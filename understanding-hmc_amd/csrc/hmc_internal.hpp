@@ -48,6 +48,7 @@ struct RandArgs {
   int n_save, traj_stride;
   int Lq, q_row0;        // q_chain buffer: rows per chain (row r at r % Lq) and the first row stored
   int d_max, on_dmax;    // NUTS (hmc_nuts.hip)
+  unsigned wait_cap;     // NUTS: wave steps a slot waits for a chain hand-off before giving up
   double* ws;            // NUTS per-chain workspace (vectors: live points, boundaries, save slots)
   const double* tape;    // NUTS replay tape [n][tape_stride] (directions / uniforms in consumption order)
   int64_t tape_stride;
@@ -129,6 +130,9 @@ hipError_t launch_rng_normals(uint32_t k0, uint32_t k1, int64_t chain0, int64_t 
 int64_t diag_rowsum_work(int64_t rows, int D);
 int64_t diag_variogram_work(int64_t n_chains, int D, int nlags);
 int64_t diag_stream_groups(int64_t n_chains);
+int64_t diag_conv_work(int64_t n_chains, int D, int T);
+hipError_t launch_conv_fused(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int64_t base, int n, int D,
+                             int T, double* work, double* out, hipStream_t st);
 hipError_t launch_stream_accum(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int D, int wrap, int slot0,
                                int carry, int rows, int64_t pos0, int n, double* shift, double* s1, double* s2, int T,
                                double* vpart, double* vsum, hipStream_t st);

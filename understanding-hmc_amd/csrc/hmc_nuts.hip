@@ -60,9 +60,17 @@ __device__ __forceinline__ double ld_wt_d(const double* p) {
   return __builtin_bit_cast(double, ld_wt(reinterpret_cast<const unsigned long long*>(p)));
 }
 
-// waves steps a slot may wait for a chain's previous iteration before the launch gives up (the
-// holder always advances, so this is only a guard against a broken hand-off)
-constexpr unsigned kMaxWaitSteps = 1u << 20;
+// Wave steps a slot may wait for a chain's previous iteration before the launch gives up (the
+// holder always advances, so this is only a guard against a broken hand-off).  Units of one chain
+// are handed out n apart, so at most ceil(slots / n) + 1 iterations of a chain are in flight and
+// each holder finishes within one tree, 2^(d_max+1) steps plus its transitions; a step of the
+// waiting wave costs about what a step of the holder's does (both run the MFMA gradient), and
+// the factor 4 covers the difference.
+inline unsigned nuts_wait_cap(int64_t slots, int64_t n, int d_max) {
+  const int64_t inflight = (slots + n - 1) / std::max<int64_t>(n, 1) + 1;
+  const int64_t cap = 4 * inflight * ((int64_t(1) << (d_max + 1)) + 64);
+  return (unsigned)std::min<int64_t>(cap, 0x7FFFFFFF);
+}
 
 // workspace vector ids (per chain).  The live points old/new (:577, :623, :750, :775) are two
 // buffers, 0 and 2 (1 and 3 are unused since the per-tree queue: no gradient is kept with them):
@@ -319,7 +327,7 @@ void k_nuts_iters(RandArgs a) {
         if (!ready) {
           ready = ld_wt(done + c) >= need;
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the state loads below the poll
-          if (!ready && ++waited > kMaxWaitSteps) {   // broken hand-off: flag it and retire the slot
+          if (!ready && ++waited > a.wait_cap) {   // broken hand-off: flag it and retire the slot
             ++n_giveup;
             state = S_DONE;
           }
@@ -679,13 +687,14 @@ void k_nuts_iters(RandArgs a) {
     if (n_unst) atomicAdd(cs + HMC_CNT_UNSTABLE, n_unst);
     if (n_dmax) atomicAdd(cs + HMC_CNT_DMAX, n_dmax);
     if (n_tape) atomicAdd(cs + HMC_CNT_OOB_REJECT, n_tape);   // NUTS: replay tape exhausted
-    if (n_giveup) atomicAdd(cs + HMC_CNT_ACCEPT, n_giveup);    // NUTS: chain hand-offs given up (must be 0)
+    if (n_giveup) atomicAdd(cs + HMC_CNT_HANDOFF_GIVEUP, n_giveup);   // broken chain hand-offs (must be 0)
     atomicAdd(cs + HMC_CNT_LEAPFROG_SQ, n_steps);               // NUTS: wave steps (lane utilisation)
   }
 }
 
 template <int MT, bool EXACT>
-hipError_t launch_nuts_mt2(const RandArgs& a, bool gen, bool replay, hipStream_t s) {
+hipError_t launch_nuts_mt2(const RandArgs& args, bool gen, bool replay, hipStream_t s) {
+  RandArgs a = args;
   // persistent: one block per CU (LDS: P + index tables), chains handed out by the queue
   const int64_t blocks = (a.n + 16 * kNutsWaves - 1) / (16 * kNutsWaves);
   const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)device_cus())));
@@ -693,6 +702,7 @@ hipError_t launch_nuts_mt2(const RandArgs& a, bool gen, bool replay, hipStream_t
   const int64_t wave_doubles = (int64_t)(V_SLOTS + 2 * (a.d_max + 1)) * 4 * MT * kWave;
   double* queue = a.ws + n_waves * wave_doubles + n_waves * 16;   // queue head, (unused), done[n]
   if (hipError_t e = hipMemsetAsync(queue, 0, nuts_queue_bytes(a.n), s)) return e;
+  a.wait_cap = nuts_wait_cap((int64_t)grid.x * kNutsWaves * 16, a.n, a.d_max);
   const size_t lds = (size_t)MT * 4 * MT * kWave * sizeof(double);
   if (a.minvf) {
     if (replay) k_nuts_iters<MT, EXACT, true, true, true><<<grid, 64 * kNutsWaves, lds, s>>>(a);

@@ -14,8 +14,8 @@ HMC_TARGET_DIAG, HMC_TARGET_DENSE = 0, 1
 HMC_RNG_REPLAY, HMC_RNG_PHILOX = 0, 1
 HMC_MODE_EXACT, HMC_MODE_FAST = 0, 1
 (CNT_ACCEPT, CNT_ACCEPT_WU, CNT_LEAPFROG, CNT_LEAPFROG_SQ, CNT_OOB_REJECT, CNT_UNSTABLE, CNT_DMAX,
- CNT_ENERGY_EVALS) = range(8)
-NCOUNTERS = 8
+ CNT_ENERGY_EVALS, CNT_HANDOFF_GIVEUP) = range(9)
+NCOUNTERS = 9
 COUNTER_SLOTS = 4096   # include/hmc.h HMC_COUNTER_SLOTS: counters buffer is [slots][NCOUNTERS]
 
 c_dp = ctypes.c_void_p  # device pointers are passed as integers (torch data_ptr())
@@ -80,6 +80,9 @@ SYMBOLS = {
     "hmc_rowsum_work_size": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
     "hmc_rowsum": (ctypes.c_int, [c_dp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                   ctypes.c_int64, ctypes.c_int32, c_dp, c_dp, c_dp, c_dp]),
+    "hmc_convergence_work_size": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
+    "hmc_convergence_sums": (ctypes.c_int, [c_dp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                            ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_dp, c_dp, c_dp]),
     "hmc_variogram_work_size": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
     "hmc_variogram": (ctypes.c_int, [c_dp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                      ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_dp, c_dp,

@@ -36,8 +36,15 @@ def _stream(t):
 
 
 def _allreduce(x, group):
+    """Sum over the ranks of `group` (RCCL over xGMI for device tensors; a gloo group -- CPU tests,
+    or several ranks sharing one GPU -- reduces a host copy)."""
     if group is not None:
-        torch.distributed.all_reduce(x, group=group)
+        if x.is_cuda and torch.distributed.get_backend(group) == "gloo":
+            h = x.cpu()
+            torch.distributed.all_reduce(h, group=group)
+            x.copy_(h)
+        else:
+            torch.distributed.all_reduce(x, group=group)
     return x
 
 
@@ -89,51 +96,104 @@ def variogram_sums(sp, t0, t1):
     return out
 
 
+def convergence_sums(sp, tmax):
+    """One pass over the samples (C-ABI hmc_convergence_sums): (3 + tmax, D) device tensor of
+    sum_j std_j, sum_j (mean_j - S), sum_j (mean_j - S)^2 and the variogram sums of lags 1..tmax,
+    S = the view's first sample (see include/hmc.h)."""
+    L = H.lib()
+    work = torch.empty(max(1, L.hmc_convergence_work_size(sp.Nchain, sp.D, tmax)), dtype=torch.float64,
+                       device=sp.t.device)
+    out = torch.empty((3 + tmax, sp.D), dtype=torch.float64, device=sp.t.device)
+    H.check(L.hmc_convergence_sums(sp.ptr, sp.Nchain, sp.cs, sp.ss, sp.base, sp.n, sp.D, tmax, H.ptr(work),
+                                   H.ptr(out), _stream(sp.t)), "hmc_convergence_sums")
+    return out
+
+
 def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
     """utils.py:77-159 on the GPU.  q_chain: (Nchain, Niter, D) NumPy array or CUDA tensor
-    (views such as q_chain_device[:, 1:, :] are read in place).  Returns (R, n_eff) NumPy."""
+    (views such as q_chain_device[:, 1:, :] are read in place).  Returns (R, n_eff) NumPy.
+
+    One pass over the samples gives every per-dimension sum R-hat needs and the variogram of lags
+    1..32 (hmc_convergence_sums); the ESS termination (utils.py:130-157) runs vectorised over the
+    dimensions on the host, and only dimensions whose criterion has not fired by then read further
+    lag blocks (hmc_variogram).  Ranks all-reduce the per-dimension sums: two rounds, B needs the
+    global mean."""
     sp = _Split(q_chain, thin_rate, warm_up_num)
-    n_local = torch.tensor([float(sp.Nchain)], dtype=torch.float64, device=sp.t.device)
-    Nchain = int(_allreduce(n_local, group).item())
-    assert Nchain > 1                                                   # utils.py:85
     n, D = sp.n, sp.D
-    m = 2 * Nchain
-    mean, std = split_moments(sp)
-    s1 = torch.stack([_rowsum(std), _rowsum(mean)])                    # sum_j std_j, sum_j mean_j
-    _allreduce(s1, group)
-    W = s1[0] / m                                                       # utils.py:112 (Q8)
-    mean_all = s1[1] / m                                                # :119
-    bsum = _allreduce(_rowsum(mean, center=mean_all), group)
+    dev = sp.t.device
+    tmax = 8 if n <= 9 else (16 if n <= 17 else 32)
+    sums = convergence_sums(sp, tmax)
+    S = sp.t.reshape(-1)[sp.base:sp.base + D].to(torch.float64)          # the kernels' shift S_d
+    m_loc = 2 * sp.Nchain
+    # round 1: sum_j std_j, sum_j mean_j (= shifted sum + m S), variogram sums, split-chain count
+    r1 = torch.cat([sums[0:1], (sums[1] + m_loc * S)[None], sums[3:],
+                    torch.full((1, D), float(m_loc), dtype=torch.float64, device=dev)])
+    _allreduce(r1, group)
+    m = int(round(float(r1[-1, 0].item())))
+    assert m > 2                                                        # Nchain > 1, utils.py:85
+    W = r1[0] / m                                                       # utils.py:112 (Q8)
+    mean_all = r1[1] / m                                                # :119
+    # round 2: sum_j (mean_j - mean_all)^2 from this rank's sums about its own shift S
+    dS = S - mean_all
+    bsum = _allreduce(sums[2] + 2.0 * dS * sums[1] + m_loc * dS * dS, group)
     B = bsum * n / float(m - 1)                                         # :120
     var = W * (n - 1) / float(n) + B / float(n)                         # :123
     R = torch.sqrt(var / W)                                             # :126
+    v = r1[2:2 + tmax].cpu().numpy()
     var_h = var.cpu().numpy()
-    # ---- ESS (utils.py:128-157): lags fetched in blocks until every dim has terminated
-    Vt = np.zeros((0, D))
-    need = np.ones(D, dtype=bool)
-    n_eff = np.zeros(D)
-    tmax = max(n - 1, 2)
-    t_done = 0
-    while True:
-        # lags required so far: 1, 2 always; more while any dim is still running
-        t1 = min(t_done + _LAG_BLOCK, tmax) + 1
-        if t1 > t_done + 1:
-            v = _allreduce(variogram_sums(sp, t_done + 1, t1), group).cpu().numpy()
-            lags = np.arange(t_done + 1, t1)
-            v = v / (m * (n - lags))[:, None]                           # utils.py:177
-            Vt = np.vstack([Vt, v])
-            t_done = t1 - 1
-        still = False
-        for i in np.nonzero(need)[0]:
-            res = _ess_dim(Vt[:, i], var_h[i], n, m, t_done >= tmax)
-            if res is None:
-                still = True
-            else:
-                n_eff[i] = res
-                need[i] = False
-        if not still:
-            break
+    # ---- ESS (utils.py:128-157), vectorised over dims; more lags only where still undecided
+    lmax = max(n - 1, 2)                                                # lags t < n exist
+    T = min(tmax, lmax)
+    Vt = v[:T] / (m * (n - np.arange(1, T + 1)))[:, None]               # utils.py:177
+    n_eff, need = ess_vectorised(Vt, var_h, n, m, complete=T >= lmax)
+    while need.any():
+        t0 = Vt.shape[0] + 1
+        t1 = min(t0 + _LAG_BLOCK, lmax + 1)
+        vb = _allreduce(variogram_sums(sp, t0, t1), group).cpu().numpy()
+        lags = np.arange(t0, t1)
+        Vt = np.vstack([Vt, vb / (m * (n - lags))[:, None]])
+        ne, need2 = ess_vectorised(Vt[:, need], var_h[need], n, m, complete=Vt.shape[0] >= lmax)
+        idx = np.nonzero(need)[0]
+        n_eff[idx[~need2]] = ne[~need2]
+        need[idx[~need2]] = False
     return R.cpu().numpy(), n_eff
+
+
+def ess_vectorised(Vt, var, n, m, complete, truncate=False):
+    """The termination loop of utils.py:130-157 for every dimension at once, given the variogram
+    values Vt[t-1, d] = V_t of lags 1..T.  Returns (n_eff, need_more): a dimension whose criterion
+    needs a lag beyond T while more lags exist (`complete` False) is flagged and its n_eff left
+    NaN; truncate=True ends such sums at T instead (streaming windows).
+
+    The reference loop (rho_k = 1 - V_k / (2 var)): if rho_1 < 0.01 (the Q9 test, sic) the sum is
+    0; otherwise for t = 1 .. n-3 it appends rho_{t+2} and stops at the first ODD t with
+    rho_{t+1} + rho_{t+2} < 0; the sum is rho_1 + ... + rho_t (t = n - 2 when it never stops,
+    NaN propagating as in np.sum), clamped at 0; n_eff = m n / (1 + 2 sum)."""
+    Vt = np.asarray(Vt, dtype=np.float64)
+    T, D = Vt.shape
+    with np.errstate(all="ignore"):
+        rho = 1.0 - Vt / (2.0 * np.asarray(var, dtype=np.float64))[None, :]
+        zero = rho[0] < 1e-2                                            # :136 (False for NaN)
+        last = n - 3                                                    # the last t the loop checks
+        avail = T - 2                                                   # checks whose lag t+2 we have
+        ts = np.arange(1, min(last, avail) + 1, 2)
+        t_stop = np.zeros(D, dtype=np.int64)
+        if ts.size:
+            hit = (rho[ts] + rho[ts + 1]) < 0                           # rho_{t+1} + rho_{t+2} < 0
+            anyh = hit.any(axis=0)
+            t_stop[anyh] = ts[hit.argmax(axis=0)[anyh]]
+        if avail >= last or complete:
+            t_none = max(n - 2, 1)                                      # ran to the end of the loop
+        else:
+            t_none = max(T - 1, 1) if truncate else 0                   # 0: more lags needed
+        t = np.where(t_stop > 0, t_stop, t_none)
+        need = ~zero & (t == 0)
+        csum = np.cumsum(rho, axis=0)                                   # csum[t-1] = rho_1 + .. + rho_t
+        ssum = csum[np.clip(t, 1, T) - 1, np.arange(D)]
+        ssum = np.where(ssum < 0, 0.0, ssum)                            # :155-156 (NaN stays NaN)
+        n_eff = np.where(zero, float(m * n), m * n / (1 + 2 * ssum))
+    n_eff[need] = np.nan
+    return n_eff, need
 
 
 def _ess_dim(Vt, var, n, m, complete, truncate=False):
@@ -240,8 +300,7 @@ def combine_split_stats(mean, std, vsum, n, group=None):
     lags = np.arange(1, T + 1)
     Vt = v / (m * (n - lags))[:, None]                                  # utils.py:177
     var_h = var.cpu().numpy()
-    n_eff = np.array([_ess_dim(Vt[:, i], var_h[i], n, m, complete=T >= n - 1, truncate=True)
-                      for i in range(D)])
+    n_eff, _ = ess_vectorised(Vt, var_h, n, m, complete=T >= n - 1, truncate=True)
     return R.cpu().numpy(), n_eff
 
 

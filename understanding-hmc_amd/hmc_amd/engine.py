@@ -88,8 +88,10 @@ class RandomEngine:
                          H.ptr(self.dE_chain), H.ptr(self.counters), H.ptr(self.traj), H.ptr(self.traj_len),
                          H.ptr(self.decision), self.n_save, self.traj_stride)
         # dense targets: scratch for L-ordered MFMA tiles (chains sorted by trajectory length
-        # every iteration; same results, no lane idling through a longer trajectory)
-        nbytes = H.lib().hmc_random_workspace_size(self.T, self.N) if order_tiles else 0
+        # every iteration; same results, no lane idling through a longer trajectory).  The large-D
+        # path (dense D > 128, diagonal D > 2048) keeps its chain state there: always allocated.
+        big = (D > 128) if kind == H.HMC_TARGET_DENSE else ((D + 1) // 2 > 16 * 64)
+        nbytes = H.lib().hmc_random_workspace_size(self.T, self.N) if (order_tiles or big) else 0
         self._order = torch.zeros((nbytes + 3) // 4, dtype=torch.int32, device=dev) if nbytes > 0 else None
         self.S.order = H.ptr(self._order)
         self._replay = None
@@ -105,7 +107,12 @@ class RandomEngine:
         self.S.qc_row0 = int(row0)
 
     def set_replay(self, p0, P, Ls, lnu):
-        """Host-replayed draws (rng='replay'): p0 (N,D), p (N,Niter,D), L (N,Niter), log u (N,Niter)."""
+        """Host-replayed draws (rng='replay'): p0 (N,D), p (N,Niter,D), L (N,Niter), log u (N,Niter).
+        L must lie in [L_low, L_high), the range np.random.randint draws it from (samplers.py:441):
+        the kernels size trajectories (and the large-D path its launch count) by L_high."""
+        Ls = np.asarray(Ls)
+        if Ls.size and (Ls.min() < self.L_low or Ls.max() >= self.L_high):
+            raise AssertionError("replay tape L outside [L_low, L_high) = [%d, %d)" % (self.L_low, self.L_high))
         dev = self.device
         self._streams = [_dev(p0, dev), _dev(P, dev), _dev(Ls, dev, torch.int32), _dev(lnu, dev)]
         self._replay = H.Replay(*[H.ptr(x) for x in self._streams], None, 0)
@@ -189,6 +196,7 @@ class RandomEngine:
         return dict(kind=type(self).__name__, N=self.N, D=self.D, n_iter=self.n_iter, warm_up=self.warm_up,
                     thin=self.thin, L_chain=self.L_chain, L_low=self.L_low, L_high=self.L_high, seed=self.seed,
                     rng=self.rng, fp_mode=self.fp_mode, chain_offset=self.chain_offset, d_max=self.d_max,
+                    order_tiles=self._order is not None,
                     dt=np.asarray(self.dt, dtype=np.float64).ravel().tolist(),
                     cov_p_sha256=hashlib.sha256(np.ascontiguousarray(self.cov_p, np.float64).tobytes()).hexdigest(),
                     target_sha256=h.hexdigest())
@@ -229,6 +237,8 @@ class RandomEngine:
                          ("ws", getattr(self, "ws", None)), ("order_ws", self._order)):
                 if t is not None and k in z.files:
                     t.copy_(torch.as_tensor(z[k]).to(self.device))
+            if self._order is not None and "order_ws" not in z.files:
+                self._order.zero_()                         # no cached gradient: recomputed from q
             if diag is not None:
                 for k, t in (("diag_shift", diag.shift), ("diag_s1", diag.s1), ("diag_s2", diag.s2),
                              ("diag_vsum", diag.vsum)):
@@ -251,9 +261,10 @@ class NutsEngine(RandomEngine):
     def __init__(self, target, n_chains, n_iter, warm_up, thin, d_max, dt, cov_p=None, rng="philox", seed=0,
                  fp_mode="fast", chain_offset=0, store_chain=True, store_energy=True, on_dmax="raise",
                  device=None):
+        # order_tiles=False: the NUTS kernel uses neither the tile order nor the gradient cache
         super().__init__(target, n_chains, n_iter, warm_up, thin, 5, 20, dt, cov_p=cov_p, rng=rng, seed=seed,
                          fp_mode=fp_mode, chain_offset=chain_offset, store_chain=store_chain,
-                         store_energy=store_energy, n_save=0, device=device, dense=True)
+                         store_energy=store_energy, n_save=0, device=device, dense=True, order_tiles=False)
         assert on_dmax in ("raise", "break")
         self.d_max = int(d_max)
         self.on_dmax = 0 if on_dmax == "raise" else 1

@@ -339,8 +339,8 @@ class HMC_sampler(sampler):
         torch.cuda.synchronize(self.device)
         elapsed = time.time() - t0
         c = eng.read_counters()
-        if c[H.CNT_ACCEPT] > 0:
-            raise RuntimeError("NUTS kernel: %d chain hand-offs timed out" % c[H.CNT_ACCEPT])
+        if c[H.CNT_HANDOFF_GIVEUP] > 0:
+            raise RuntimeError("NUTS kernel: %d chain hand-offs timed out" % c[H.CNT_HANDOFF_GIVEUP])
         if c[H.CNT_OOB_REJECT] > 0:
             raise IndexError("NUTS replay tape exhausted")
         if c[H.CNT_DMAX] > 0 and on_dmax == "raise":

@@ -17,6 +17,24 @@ def start_pts(q0, cov0, size):
     return np.random.multivariate_normal(q0, cov0, size=size)
 
 
+START_ITERATION = 0x7FFFFFFF   # Philox iteration word reserved for start points (no run reaches it)
+
+
+def start_pts_device(seed, chain0, n, D, scale=np.sqrt(2.0), device=None):
+    """utils.py:204-209 for many chains on the device: q_start[c] = scale * z, z ~ N(0, I_D), keyed
+    by (seed, GLOBAL chain id chain0 + c) through the kernels' Philox4x32-10 + Box-Muller (C-ABI
+    hmc_rng_normals, iteration word START_ITERATION), so a chain starts from the same point
+    whichever shard or GPU count holds it.  Returns an (n, D) float64 device tensor."""
+    import torch
+    from . import _lib as H
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    npairs = (int(D) + 1) // 2
+    out = torch.empty((int(n), 2 * npairs), dtype=torch.float64, device=dev)
+    H.check(H.lib().hmc_rng_normals(int(seed), int(chain0), int(n), START_ITERATION, npairs, H.ptr(out),
+                                    torch.cuda.current_stream(dev).cuda_stream), "hmc_rng_normals")
+    return (out[:, :D] * float(scale)).contiguous()
+
+
 def normal_lnL(q, q0, cov0):
     """utils.py:213-218."""
     return multivariate_normal.logpdf(q, mean=q0, cov=cov0)
