@@ -456,12 +456,14 @@ def main():
             n_samples, t_samples = R, t_max * R / float(timed_rows)
         torch.cuda.synchronize(dev)
         diag_s = time.perf_counter() - td
+        from hmc_amd.diagnostics import LAST_INFO
         ess = dict(ess_per_s_median=float(np.median(neff)) / t_samples,
                    ess_per_s_min=float(np.min(neff)) / t_samples,
                    ess_per_s_median_incl_diag=float(np.median(neff)) / (t_samples + (0.0 if sd else diag_s)),
                    n_eff_median=float(np.median(neff)), n_eff_min=float(np.min(neff)),
                    rhat_median=float(np.median(R_hat)), rhat_max=float(np.max(R_hat)),
                    samples_per_chain=n_samples, sampling_s=t_samples, diagnostics_s=diag_s,
+                   diagnostics_lags=None if sd is not None else dict(LAST_INFO),
                    method=(f"streaming statistics (tmax={a.tmax}) over every timed sample, fed inside the timed loop"
                            if sd is not None else
                            f"reference estimator on the circular window's last {R} samples per chain (all chains), "

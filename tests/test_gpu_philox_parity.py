@@ -238,7 +238,9 @@ def test_wave_c4_shard_full_shape():
     assert np.abs(x.mean(axis=0)).max() < 6 / np.sqrt(N)
     assert np.abs(x.var(axis=0) - 1).max() < 6 * np.sqrt(2 / N)
     R, neff = sd_all.finish()
-    assert np.all(np.isfinite(R)) and np.all(np.abs(R - 1) < 0.01)
+    # n = 14 samples per split half: the reference's R-hat mixes W = mean of stds (Q8) with B, so
+    # stationary chains sit near sqrt((n-1)/n + B/(n W)) ~ 1.04 here, the same in every dimension
+    assert np.all(np.isfinite(R)) and np.all(np.abs(R - 1) < 0.1) and R.std() < 0.01
     assert np.all(neff > 0)
     cut = N // 2 + 40
     qa, ca, sa = run(0, cut)

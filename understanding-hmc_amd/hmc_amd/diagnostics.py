@@ -146,17 +146,32 @@ def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
     T = min(tmax, lmax)
     Vt = v[:T] / (m * (n - np.arange(1, T + 1)))[:, None]               # utils.py:177
     n_eff, need = ess_vectorised(Vt, var_h, n, m, complete=T >= lmax)
-    while need.any():
-        t0 = Vt.shape[0] + 1
-        t1 = min(t0 + _LAG_BLOCK, lmax + 1)
-        vb = _allreduce(variogram_sums(sp, t0, t1), group).cpu().numpy()
-        lags = np.arange(t0, t1)
-        Vt = np.vstack([Vt, vb / (m * (n - lags))[:, None]])
-        ne, need2 = ess_vectorised(Vt[:, need], var_h[need], n, m, complete=Vt.shape[0] >= lmax)
+    LAST_INFO.update(tmax=tmax, lags=T, fallback_dims=int(need.sum()), fallback_passes=0)
+    if need.any():
+        # the dims whose criterion reads lags > T: gather their columns once (one strided read of
+        # the lines holding them) into a compact (N, 2n, k) copy, and run the lag blocks on it (the
+        # all-reduced sums make `need` the same on every rank)
         idx = np.nonzero(need)[0]
-        n_eff[idx[~need2]] = ne[~need2]
-        need[idx[~need2]] = False
+        view = sp.t[:, warm_up_num::thin_rate, :][:, :2 * n, :]
+        sub_t = view.index_select(2, torch.as_tensor(idx, device=dev)).contiguous()
+        ssp = _Split(sub_t, 1, 0)
+        Vs = Vt[:, idx]
+        while True:
+            t0 = Vs.shape[0] + 1
+            t1 = min(t0 + _LAG_BLOCK, lmax + 1)
+            vb = _allreduce(variogram_sums(ssp, t0, t1), group).cpu().numpy()
+            LAST_INFO["fallback_passes"] += 1
+            lags = np.arange(t0, t1)
+            Vs = np.vstack([Vs, vb / (m * (n - lags))[:, None]])
+            ne, need2 = ess_vectorised(Vs, var_h[idx], n, m, complete=Vs.shape[0] >= lmax)
+            if not need2.any():
+                break
+        n_eff[idx] = ne
+        LAST_INFO["lags"] = Vs.shape[0]
     return R.cpu().numpy(), n_eff
+
+
+LAST_INFO = {}   # what the last convergence_stats call read: fused lags, fallback dims and passes
 
 
 def ess_vectorised(Vt, var, n, m, complete, truncate=False):
