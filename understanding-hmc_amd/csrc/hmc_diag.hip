@@ -170,7 +170,12 @@ __global__ __launch_bounds__(256) void k_variogram_ring(Src s, int t0, int nt, i
 
 // ---- ONE pass for convergence_stats (utils.py:88-126 and :161-179).  Per split chain j (n samples)
 // and dim d, with y = x - x_j[0] (shifted: the sums stay well conditioned):
-//   s1 = sum y, s2 = sum y^2  ->  mean_j = x_j[0] + s1/n, std_j = sqrt((s2 - s1 s1/n)/(n - 1))
+//   mean_j = (x[0] + x[1] + ... + x[n-1]) / n, summed in sample order without FMA: NumPy's np.mean
+//   over axis 0 bit for bit (np.std(ddof=1) at utils.py:109-112 starts from it);
+//   s1 = sum y, s2 = sum y^2, delta = mean_j - x_j[0]:
+//   sum (x - mean_j)^2 = s2 - 2 delta s1 + n delta^2 (NumPy's second pass, up to rounding: for a chain
+//   that never moved, e.g. every proposal rejected, it is n delta^2 with NumPy's own delta, so
+//   W = mean std_j keeps the reference's rounding-level value instead of an exact 0)
 //   V_t,j = sum_{s<n-t} (y[s+t] - y[s])^2 = 2 s2 - P_t - Q_t - 2 C_t,  C_t = sum_s y[s] y[s+t],
 //   P_t = sum_{s<t} y^2 (the first t samples), Q_t = sum_{s>=n-t} y^2 (the last t)
 // so a lag costs ONE FMA per sample (v[t] += (-2 y[s]) y[s-t-1] against a register ring of the last
@@ -206,12 +211,14 @@ __global__ __launch_bounds__(256) void k_conv_fused(Src s, int groups, int ntile
       double ring[T];
 #pragma unroll
       for (int k = 0; k < T; ++k) ring[k] = 0.0;
-      double s1 = 0.0, s2 = 0.0;
+      double s1 = 0.0, s2 = 0.0, r1 = 0.0;
       // first T samples: their running sum of squares gives P_t (lag t = i + 1)
 #pragma unroll
       for (int i = 0; i < T; ++i) {
         if (i < n) {
-          const double y = bp[(int64_t)i * ss] - sh;
+          const double x = bp[(int64_t)i * ss];
+          r1 += x;
+          const double y = x - sh;
           s1 += y;
           s2 = __builtin_fma(y, y, s2);
           const double ym2 = -2.0 * y;
@@ -230,6 +237,7 @@ __global__ __launch_bounds__(256) void k_conv_fused(Src s, int groups, int ntile
 #pragma unroll
         for (int u = 0; u < kConvUnroll; ++u) {
           if (i0 + u < n) {                       // uniform
+            r1 += xs[u];
             const double y = xs[u] - sh;
             s1 += y;
             s2 = __builtin_fma(y, y, s2);
@@ -250,10 +258,11 @@ __global__ __launch_bounds__(256) void k_conv_fused(Src s, int groups, int ntile
         q = __builtin_fma(ring[t], ring[t], q);
         v[t] += s2x2 - q;
       }
-      const double mu = s1 / n;
-      const double var = (s2 - s1 * mu) / (n - 1);
-      a_std += sqrt(var > 0.0 ? var : 0.0);
-      const double e = (sh - S) + mu;
+      const double mean = r1 / n;
+      const double dl = mean - sh;
+      const double m2 = (s2 - 2.0 * dl * s1) + n * (dl * dl);
+      a_std += sqrt(m2 > 0.0 ? m2 / (n - 1) : 0.0);
+      const double e = mean - S;
       a_m += e;
       a_m2 = __builtin_fma(e, e, a_m2);
     }
