@@ -326,7 +326,7 @@ hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_s
   if (replay && (!r || !r->p || !r->tape || r->tape_stride < 1)) return fail(HMC_EINVAL, "replay mode needs p and tape");
   if (s->n_chains == 0 || s->iter_end == s->iter_begin) return HMC_OK;
   if (!workspace) return fail(HMC_EINVAL, "null workspace");
-  const hmc::Layout lay{0, 0, 0, (t->D + 1) / 2};
+  const hmc::Layout lay{0, 0, 16, (t->D + 1) / 2};   // 16 chain slots per wave (debug stamps: one row per wave)
   hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
   a.d_max = s->d_max;
   a.on_dmax = s->on_dmax;

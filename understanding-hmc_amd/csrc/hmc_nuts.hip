@@ -81,6 +81,23 @@ enum : int { V_OLD_Q = 0, V_OLD_G = 1, V_NEW_Q = 2, V_NEW_G = 3, V_LEFT_Q = 4, V
 
 __device__ __forceinline__ int nuts_nvec(int d_max) { return V_SLOTS + 2 * (d_max + 1); }
 
+// Phase timers of the debug build (make debug; HMC_DEBUG_STAMPS): wave-uniform s_memtime deltas per
+// part of a wave step, summed over the launch: 0 transitions, 1 half kick + drift, 2 gradient
+// (MFMA), 3 half kick + energies, 4 new-point bookkeeping / saves, 5 loaded U-turn checks,
+// 6 progressive sampling, 7 sub-tree end.  The release library compiles none of it.
+#ifdef HMC_DEBUG_HOOKS
+#define NUTS_PHASE(i)                                        \
+  do {                                                       \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    ph[i] += t_ - t_ph;                                      \
+    t_ph = t_;                                               \
+  } while (0)
+#else
+#define NUTS_PHASE(i) \
+  do {                \
+  } while (0)
+#endif
+
 // bytes of the work queue block, zeroed before every launch: head, a spare word, done[n] (u32),
 // padded to a multiple of 16
 inline size_t nuts_queue_bytes(int64_t n) { return (size_t)((16 + 4 * n + 15) / 16 * 16); }
@@ -258,6 +275,10 @@ void k_nuts_iters(RandArgs a) {
   int64_t tpos = 0;                                     // replay tape cursor (persists across launches)
   int old2 = 0;                                         // vector offset of the live_point_old pair
   unsigned long long n_lf = 0, n_unst = 0, n_dmax = 0, n_tape = 0, n_steps = 0, n_giveup = 0;
+#ifdef HMC_DEBUG_HOOKS
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_ph = __builtin_amdgcn_s_memtime();
+#endif
 
   auto draw = [&](bool direction) -> double {           // next random number of this chain (reference order)
     if constexpr (REPLAY) {
@@ -441,6 +462,7 @@ void k_nuts_iters(RandArgs a) {
       }
     }
     if (!__builtin_amdgcn_ballot_w64(state != S_DONE)) break;
+    NUTS_PHASE(0);
 
     // ================= one leapfrog for every chain inside a sub-tree (:612-614, :639)
     // chains outside a sub-tree are frozen by the EXEC mask of a divergent block (no per-dim
@@ -472,7 +494,9 @@ void k_nuts_iters(RandArgs a) {
         if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
     }
+    NUTS_PHASE(1);
     gradient<MT, GEN, true, SHORT>(a, sP, lane, h, q, acc);
+    NUTS_PHASE(2);
     if (act) {
 #pragma unroll
       for (int m = 0; m < M; ++m) {
@@ -515,6 +539,7 @@ void k_nuts_iters(RandArgs a) {
     }
     if (act && h == 0) ++n_lf;
     ++n_steps;
+    NUTS_PHASE(3);
 
     // ================= process the new point
     bool reject = false, sub_end = false;
@@ -539,6 +564,7 @@ void k_nuts_iters(RandArgs a) {
         vstore<M>(W, V_SLOTS + 1, 2 * s, p);
       }
     }
+    NUTS_PHASE(4);
     // even point: sub-tree U-turn checks against check_points(mpt) (:699-736), converged loop
     const bool checking = later && !reject && (mpt & 1) == 0;
     {                                                   // the check against point mpt - 1, from registers
@@ -588,6 +614,7 @@ void k_nuts_iters(RandArgs a) {
         }                                               // (release, :735-736: nothing to free)
       }
     }
+    NUTS_PHASE(5);
     if (later && !reject) {                             // progressive sampling (:743-751)
       const double E_max_prev = E_max_now;
       E_max_now = fmax(E_max_prev, E_tmp);
@@ -607,6 +634,7 @@ void k_nuts_iters(RandArgs a) {
       sub_end = k == Lsub;
     }
     if (act && reject) state = S_ITER_END;               // q = live_point_q_old (:649, :731)
+    NUTS_PHASE(6);
 
     // ================= sub-tree end: boundary, biased acceptance, termination (:757-784)
     // The other end (q, p, g) is loaded here for the termination dots; a next doubling towards it
@@ -670,7 +698,14 @@ void k_nuts_iters(RandArgs a) {
         state = S_READY;
       }
     }
+    NUTS_PHASE(7);
   }
+#ifdef HMC_DEBUG_HOOKS
+  if (a.stamps && lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a.stamps[wv * 8 + i] = ph[i];
+  }
+#endif
 
   // counters (every chain's state was written back when its slot fetched the next one)
   n_lf = wave_sum_u64(n_lf);
