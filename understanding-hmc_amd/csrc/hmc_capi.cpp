@@ -433,8 +433,10 @@ hmc_status hmc_variogram(const double* x, int64_t n_chains, int64_t chain_stride
                     "hmc_variogram");
 }
 
+static bool conv_tmax_ok(int32_t t) { return t == 8 || t == 16 || t == 32 || t == 64; }
+
 int64_t hmc_convergence_work_size(int64_t n_chains, int32_t D, int32_t tmax) {
-  if (n_chains < 1 || D < 1 || (tmax != 8 && tmax != 16 && tmax != 32)) return 0;
+  if (n_chains < 1 || D < 1 || !conv_tmax_ok(tmax)) return 0;
   return hmc::diag_conv_work(n_chains, D, tmax);
 }
 
@@ -442,7 +444,7 @@ hmc_status hmc_convergence_sums(const double* x, int64_t n_chains, int64_t chain
                                 int64_t base, int32_t n, int32_t D, int32_t tmax, double* work, double* out,
                                 void* stream) {
   if (!x || !work || !out || n_chains < 1 || n < 2 || D < 1) return fail(HMC_EINVAL, "bad arguments");
-  if (tmax != 8 && tmax != 16 && tmax != 32) return fail(HMC_EINVAL, "tmax must be 8, 16 or 32");
+  if (!conv_tmax_ok(tmax)) return fail(HMC_EINVAL, "tmax must be 8, 16, 32 or 64");
   return hip_status(hmc::launch_conv_fused(x, n_chains, chain_stride, sample_stride, base, n, D, tmax, work, out,
                                            (hipStream_t)stream),
                     "hmc_convergence_sums");

@@ -172,113 +172,117 @@ __global__ __launch_bounds__(256) void k_variogram_ring(Src s, int t0, int nt, i
 // and dim d, with y = x - x_j[0] (shifted: the sums stay well conditioned):
 //   mean_j = (x[0] + x[1] + ... + x[n-1]) / n, summed in sample order without FMA: NumPy's np.mean
 //   over axis 0 bit for bit (np.std(ddof=1) at utils.py:109-112 starts from it);
-//   s1 = sum y, s2 = sum y^2, delta = mean_j - x_j[0]:
-//   sum (x - mean_j)^2 = s2 - 2 delta s1 + n delta^2 (NumPy's second pass, up to rounding: for a chain
+//   s1 = sum y, S2 = sum y^2, delta = mean_j - x_j[0]:
+//   sum (x - mean_j)^2 = S2 - 2 delta s1 + n delta^2 (NumPy's second pass, up to rounding: for a chain
 //   that never moved, e.g. every proposal rejected, it is n delta^2 with NumPy's own delta, so
 //   W = mean std_j keeps the reference's rounding-level value instead of an exact 0)
-//   V_t,j = sum_{s<n-t} (y[s+t] - y[s])^2 = 2 s2 - P_t - Q_t - 2 C_t,  C_t = sum_s y[s] y[s+t],
-//   P_t = sum_{s<t} y^2 (the first t samples), Q_t = sum_{s>=n-t} y^2 (the last t)
-// so a lag costs ONE FMA per sample (v[t] += (-2 y[s]) y[s-t-1] against a register ring of the last
-// T samples) instead of a subtraction and an FMA.  Sums over the block's split chains:
+//   V_t,j = sum_{s<n-t} (y[s+t] - y[s])^2 = 2 S2 - H_t - T_t - 2 C_t,  C_t = sum_s y[s] y[s-t],
+//   H_t = sum_{s<t} y^2 (the first t samples), T_t = sum_{s>=n-t} y^2 (the last t)
+// so a lag costs ONE FMA per sample (v += (-2 y[s]) y[s-t] against a register ring) instead of a
+// subtraction and an FMA.  The lags are split over G waves (lag group g: lags gTW+1 .. gTW+TW, a
+// ring fed by the sample stream delayed by gTW), so T = G*TW lags fit the register file:
+//   * samples run in chunks of TW; chunk g is exactly the positions whose running S2 is H_t of
+//     this wave's lags (static register index inside the unrolled chunk);
+//   * at the end the ring holds y[n-1-gTW-k], so T_t = (S2 - S2 through position n-1-gTW) +
+//     cumulative squares of the ring.
+// Sums over the block's split chains:
 //   row 0: sum_j std_j, row 1: sum_j (mean_j - S_d), row 2: sum_j (mean_j - S_d)^2,
 //   row 3 + t - 1: sum_j V_t,j for lags t = 1..T (valid for t < n), S_d = x[base + d].
-// Block = 4 split-chain rows x 64 dims (lane = dim: coalesced rows).  The dim tiles of one chain
-// group run on the same XCD (block b on XCD b % 8), so a row's line shared by two tiles is fetched
-// from HBM once.
-constexpr int kConvUnroll = 8;
-
-template <int T>
-__global__ __launch_bounds__(256) void k_conv_fused(Src s, int groups, int ntiles, double* partial) {
+// Block = 4 waves = 4/G split chains at a time x G lag groups, lane = dim (coalesced rows).  The dim
+// tiles of one chain group run on the same XCD (block b on XCD b % 8), so a row's line shared by
+// two tiles is fetched from HBM once.
+template <int TW, int G>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_conv_lags(Src s, int groups,
+                                                                                             int ntiles,
+                                                                                             double* partial) {
+  constexpr int SL = 4 / G;             // split chains per block at a time
+  constexpr int T = TW * G;
   __shared__ double red[4][kDimTile];
   const int dl = threadIdx.x & (kDimTile - 1);
-  const int rl = threadIdx.x / kDimTile;
-  const int b = blockIdx.x;                       // XCD-aware: tiles of a group 8 blocks apart
+  const int w = threadIdx.x / kDimTile;
+  const int slot = w / G, g = w % G;    // wave-uniform
+  const int gofs = g * TW;              // this wave's lags: gofs + 1 .. gofs + TW
+  const int b = blockIdx.x;             // XCD-aware: tiles of a group 8 blocks apart
   const int tile = (b >> 3) % ntiles;
   const int grp = (b & 7) + 8 * ((b >> 3) / ntiles);
   const int d = tile * kDimTile + dl;
   const int64_t m2 = 2 * s.n_chains;
   const int64_t ss = s.sample_stride;
   const int n = s.n;
-  double v[T];
+  double v[TW];
 #pragma unroll
-  for (int t = 0; t < T; ++t) v[t] = 0.0;
+  for (int k = 0; k < TW; ++k) v[k] = 0.0;
   double a_std = 0.0, a_m = 0.0, a_m2 = 0.0;
   if (d < s.D && grp < groups) {
     const double S = s.x[s.base + d];
-    for (int64_t j = (int64_t)grp * 4 + rl; j < m2; j += (int64_t)groups * 4) {
+    const int pos_suf = n - gofs - 1;   // T_t needs S2 through this position
+    for (int64_t j = (int64_t)grp * SL + slot; j < m2; j += (int64_t)groups * SL) {
       const double* bp = split_ptr(s, j, 0) + d;
       const double sh = bp[0];
-      double ring[T];
+      double ring[TW];
 #pragma unroll
-      for (int k = 0; k < T; ++k) ring[k] = 0.0;
-      double s1 = 0.0, s2 = 0.0, r1 = 0.0;
-      // first T samples: their running sum of squares gives P_t (lag t = i + 1)
+      for (int k = 0; k < TW; ++k) ring[k] = 0.0;
+      double s1 = 0.0, s2 = 0.0, r1 = 0.0, sufb = 0.0;
+      for (int c0 = 0; c0 < n; c0 += TW) {
+        double xc[TW], xd[TW];
 #pragma unroll
-      for (int i = 0; i < T; ++i) {
-        if (i < n) {
-          const double x = bp[(int64_t)i * ss];
-          r1 += x;
-          const double y = x - sh;
-          s1 += y;
-          s2 = __builtin_fma(y, y, s2);
-          const double ym2 = -2.0 * y;
-#pragma unroll
-          for (int t = 0; t < i; ++t) v[t] = __builtin_fma(ym2, ring[t], v[t]);
-          v[i] -= s2;
-#pragma unroll
-          for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
-          ring[0] = y;
+        for (int i = 0; i < TW; ++i) {
+          const int sp = c0 + i, sq = sp - gofs;
+          xc[i] = sp < n ? bp[(int64_t)sp * ss] : 0.0;
+          xd[i] = (sq >= 0 && sq < n) ? bp[(int64_t)sq * ss] : sh;   // delayed stream (y = 0 before 0)
         }
-      }
-      for (int i0 = T; i0 < n; i0 += kConvUnroll) {
-        double xs[kConvUnroll];
+        const bool hwin = c0 == gofs;   // uniform: this chunk's running S2 gives H_t of our lags
 #pragma unroll
-        for (int u = 0; u < kConvUnroll; ++u) xs[u] = (i0 + u < n) ? bp[(int64_t)(i0 + u) * ss] : 0.0;
-#pragma unroll
-        for (int u = 0; u < kConvUnroll; ++u) {
-          if (i0 + u < n) {                       // uniform
-            r1 += xs[u];
-            const double y = xs[u] - sh;
+        for (int i = 0; i < TW; ++i) {
+          const int sp = c0 + i;
+          if (sp < n) {                 // uniform
+            r1 += xc[i];
+            const double y = xc[i] - sh;
             s1 += y;
             s2 = __builtin_fma(y, y, s2);
             const double ym2 = -2.0 * y;
 #pragma unroll
-            for (int t = 0; t < T; ++t) v[t] = __builtin_fma(ym2, ring[t], v[t]);
+            for (int k = 0; k < TW; ++k) v[k] = __builtin_fma(ym2, ring[k], v[k]);
+            if (hwin) v[i] -= s2;       // H_t, t = gofs + 1 + i
+            if (sp == pos_suf) sufb = s2;
 #pragma unroll
-            for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
-            ring[0] = y;
+            for (int k = TW - 1; k > 0; --k) ring[k] = ring[k - 1];
+            ring[0] = xd[i] - sh;       // y[sp - gofs]
           }
         }
       }
-      // the last T samples (ring[k] = y[n-1-k]) give Q_t; every lag gets 2 s2
-      double q = 0.0;
+      // ring[k] = y[n-1-gofs-k]: T_t = (S2 - S2 through n-1-gofs) + sum_{k' <= k} ring[k']^2
+      double q = pos_suf >= 0 ? s2 - sufb : s2;
       const double s2x2 = 2.0 * s2;
 #pragma unroll
-      for (int t = 0; t < T; ++t) {
-        q = __builtin_fma(ring[t], ring[t], q);
-        v[t] += s2x2 - q;
+      for (int k = 0; k < TW; ++k) {
+        q = __builtin_fma(ring[k], ring[k], q);
+        v[k] += s2x2 - q;
       }
       const double mean = r1 / n;
-      const double dl = mean - sh;
-      const double m2 = (s2 - 2.0 * dl * s1) + n * (dl * dl);
-      a_std += sqrt(m2 > 0.0 ? m2 / (n - 1) : 0.0);
+      const double dm = mean - sh;
+      const double mm2 = (s2 - 2.0 * dm * s1) + n * (dm * dm);
+      a_std += sqrt(mm2 > 0.0 ? mm2 / (n - 1) : 0.0);
       const double e = mean - S;
       a_m += e;
       a_m2 = __builtin_fma(e, e, a_m2);
     }
   }
   auto put = [&](int row, double x) {
-    red[rl][dl] = x;
+    red[w][dl] = x;
     __syncthreads();
-    if (rl == 0 && d < s.D && grp < groups)
+    if (w == 0 && d < s.D && grp < groups)
       partial[((int64_t)grp * (T + 3) + row) * s.D + d] = ((red[0][dl] + red[1][dl]) + red[2][dl]) + red[3][dl];
     __syncthreads();
   };
-  put(0, a_std);
-  put(1, a_m);
-  put(2, a_m2);
+  put(0, g == 0 ? a_std : 0.0);
+  put(1, g == 0 ? a_m : 0.0);
+  put(2, g == 0 ? a_m2 : 0.0);
 #pragma unroll
-  for (int t = 0; t < T; ++t) put(3 + t, v[t]);
+  for (int gg = 0; gg < G; ++gg) {
+#pragma unroll
+    for (int k = 0; k < TW; ++k) put(3 + gg * TW + k, g == gg ? v[k] : 0.0);
+  }
 }
 
 // ---- streaming (windowed) split-chain statistics: q_chain never has to be stored whole.
@@ -451,10 +455,11 @@ hipError_t launch_conv_fused(const double* x, int64_t n_chains, int64_t cs, int6
   // blocks: 8 groups x ntiles per 8 * ntiles consecutive block ids (XCD-aware order, see kernel)
   const int64_t gpad = (groups + 7) / 8 * 8;
   const dim3 grid((unsigned)(gpad * ntiles));
-  switch (T) {
-    case 8: k_conv_fused<8><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
-    case 16: k_conv_fused<16><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
-    case 32: k_conv_fused<32><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
+  switch (T) {   // T = TW x G lags
+    case 8: k_conv_lags<8, 1><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
+    case 16: k_conv_lags<16, 1><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
+    case 32: k_conv_lags<16, 2><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
+    case 64: k_conv_lags<16, 4><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
     default: return hipErrorInvalidValue;
   }
   if (hipError_t e = hipGetLastError()) return e;

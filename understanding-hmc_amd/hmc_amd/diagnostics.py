@@ -113,15 +113,15 @@ def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
     """utils.py:77-159 on the GPU.  q_chain: (Nchain, Niter, D) NumPy array or CUDA tensor
     (views such as q_chain_device[:, 1:, :] are read in place).  Returns (R, n_eff) NumPy.
 
-    One pass over the samples gives every per-dimension sum R-hat needs and the variogram of lags
-    1..32 (hmc_convergence_sums); the ESS termination (utils.py:130-157) runs vectorised over the
-    dimensions on the host, and only dimensions whose criterion has not fired by then read further
-    lag blocks (hmc_variogram).  Ranks all-reduce the per-dimension sums: two rounds, B needs the
+    One pass over the samples gives every per-dimension sum R-hat needs and the variogram of every
+    lag t < n up to 64 (hmc_convergence_sums); the ESS termination (utils.py:130-157) runs vectorised
+    over the dimensions on the host, and only dimensions whose criterion has not fired by then
+    (n > 65 and slow mixing) read further lag blocks (hmc_variogram).  Ranks all-reduce the per-dimension sums: two rounds, B needs the
     global mean."""
     sp = _Split(q_chain, thin_rate, warm_up_num)
     n, D = sp.n, sp.D
     dev = sp.t.device
-    tmax = 8 if n <= 9 else (16 if n <= 17 else 32)
+    tmax = next((t for t in (8, 16, 32, 64) if t >= n - 1), 64)   # all lags t < n when they fit
     sums = convergence_sums(sp, tmax)
     S = sp.t.reshape(-1)[sp.base:sp.base + D].to(torch.float64)          # the kernels' shift S_d
     m_loc = 2 * sp.Nchain
@@ -152,9 +152,13 @@ def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
         # the lines holding them) into a compact (N, 2n, k) copy, and run the lag blocks on it (the
         # all-reduced sums make `need` the same on every rank)
         idx = np.nonzero(need)[0]
-        view = sp.t[:, warm_up_num::thin_rate, :][:, :2 * n, :]
-        sub_t = view.index_select(2, torch.as_tensor(idx, device=dev)).contiguous()
-        ssp = _Split(sub_t, 1, 0)
+        if 4 * idx.size <= D:
+            view = sp.t[:, warm_up_num::thin_rate, :][:, :2 * n, :]
+            sub_t = view.index_select(2, torch.as_tensor(idx, device=dev)).contiguous()
+            ssp = _Split(sub_t, 1, 0)
+        else:                                    # most dims: read the samples in place instead
+            ssp = sp
+            idx = np.arange(D)
         Vs = Vt[:, idx]
         while True:
             t0 = Vs.shape[0] + 1
