@@ -133,7 +133,8 @@ hmc::RandArgs rand_args(const hmc_target* t, const hmc_kinetic* k, const hmc_sch
   if (const char* ab = getenv("HMC_DEBUG_ABLATE")) a.dbg = atoi(ab);
   if (const char* dl = getenv("HMC_DEBUG_L")) a.dbgL = atoi(dl);
   if (getenv("HMC_DEBUG_STAMPS")) {                                     // diagnostic phase timers
-    const int64_t waves = (s->n_chains + lay.cpw - 1) / lay.cpw;
+    const int cpw = lay.cpw > 0 ? lay.cpw : 16;   // dense / NUTS layouts: 16 chains per wave
+    const int64_t waves = (s->n_chains + cpw - 1) / cpw;
     if (g_stamps) (void)hipFree(g_stamps);
     g_stamps = nullptr;
     g_stamp_waves = waves;

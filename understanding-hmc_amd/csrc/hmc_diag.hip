@@ -306,9 +306,11 @@ struct StreamArgs {
 constexpr int kStreamChunk = 8;   // window rows loaded together (memory-level parallelism)
 
 // Block = 4 chain lanes x 64 dims (lane = dim: coalesced rows).  Each thread walks its chains'
-// new rows once, with the last T samples in a register ring: per element, T differences.
-// T <= 16 capped at 168 registers: three waves per SIMD keep enough rows in flight (the
-// kernel is HBM-bound; two waves per SIMD measured 10% slower).
+// new rows once, with the last T shifted samples in a register ring: per element ONE FMA per lag
+// (the product form of k_conv_lags: V_t = 2 S2 - H_t - T_t - 2 C_t; the H_t / T_t terms and the
+// same-half masks only in rows within T of a half's start or end, 2 S2 when a half completes, so
+// vsum holds the variogram sums of every completed half).
+// T <= 16 capped at 168 registers: three waves per SIMD keep enough rows in flight.
 template <int T>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T <= 16 ? 3 : 1))) void k_stream_accum(StreamArgs a) {
   __shared__ double red[4][kDimTile];
@@ -328,13 +330,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T <= 16 ? 3
         sl = sl >= a.wrap ? sl - a.wrap : sl;
         return xc[(int64_t)sl * a.sample_stride];
       };
-      double ring[T];
-#pragma unroll
-      for (int k = 0; k < T; ++k) ring[k] = (k < a.carry) ? at(a.carry - 1 - k) : 0.0;
       const int64_t o = c * 2 * a.D + d;
       double sh[2] = {a.shift[o], a.shift[o + a.D]};
       double m1[2] = {a.s1[o], a.s1[o + a.D]};
       double m2[2] = {a.s2[o], a.s2[o + a.D]};
+      // ring of shifted samples y = x - shift of the first new row's half (carry rows of the other
+      // half are never multiplied: lags are masked to the same half below)
+      const int hc = a.pos0 >= a.n ? 1 : 0;
+      double ring[T];
+#pragma unroll
+      for (int k = 0; k < T; ++k) ring[k] = (k < a.carry) ? at(a.carry - 1 - k) - sh[hc] : 0.0;
       for (int i0 = 0; i0 < rows; i0 += kStreamChunk) {
         double xs[kStreamChunk];
 #pragma unroll
@@ -344,43 +349,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T <= 16 ? 3
         const int64_t p0 = a.pos0 + i0;
         const int h0 = p0 >= a.n ? 1 : 0;
         const int64_t s0 = p0 - (int64_t)h0 * a.n;
-        if (i0 + kStreamChunk <= rows && s0 >= T && s0 + kStreamChunk <= a.n) {
+        if (i0 + kStreamChunk <= rows && s0 >= T && s0 + kStreamChunk <= a.n - T) {
 #pragma unroll
           for (int j = 0; j < kStreamChunk; ++j) {
-            const double x = xs[j];
-            const double e = x - sh[h0];
-            m1[h0] += e;
-            m2[h0] = __builtin_fma(e, e, m2[h0]);
+            const double y = xs[j] - sh[h0];
+            m1[h0] += y;
+            m2[h0] = __builtin_fma(y, y, m2[h0]);
+            const double ym2 = -2.0 * y;
 #pragma unroll
-            for (int t = 0; t < T; ++t) {
-              const double df = x - ring[t];
-              v[t] = __builtin_fma(df, df, v[t]);
-            }
+            for (int t = 0; t < T; ++t) v[t] = __builtin_fma(ym2, ring[t], v[t]);   // -2 C_t
 #pragma unroll
             for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
-            ring[0] = x;
+            ring[0] = y;
           }
           continue;
         }
-#pragma unroll
+        // rows within T of a half's start or end (rare: not unrolled, the row re-read from cache):
+        // same-half lag masks, the H_t / T_t terms of V_t = 2 S2 - H_t - T_t - 2 C_t, and 2 S2 once
+        // the half is complete (see k_conv_lags)
+#pragma unroll 1
         for (int j = 0; j < kStreamChunk; ++j) {
           if (i0 + j >= rows) break;
-          const double x = xs[j];
           const int64_t p = a.pos0 + i0 + j;
           const int h = p >= a.n ? 1 : 0;
           const int sidx = (int)(p - (int64_t)h * a.n);
-          if (sidx == 0) sh[h] = x;
-          const double e = x - sh[h];
-          m1[h] += e;
-          m2[h] = __builtin_fma(e, e, m2[h]);
+          const double xj = at(a.carry + i0 + j);
+          if (sidx == 0) sh[h] = xj;
+          const double y = xj - sh[h];
+          m1[h] += y;
+          m2[h] = __builtin_fma(y, y, m2[h]);
+          const double ym2 = -2.0 * y, y2 = y * y;
+          const int tail = a.n - 1 - sidx;      // lags t+1 >= n - sidx count this sample in T_t
 #pragma unroll
           for (int t = 0; t < T; ++t) {
-            const double df = x - ring[t];
-            v[t] = (t < sidx) ? __builtin_fma(df, df, v[t]) : v[t];   // lag t+1 inside the same half
+            double vt = (t < sidx) ? __builtin_fma(ym2, ring[t], v[t]) : v[t];   // lag t+1 inside the half
+            vt = (t >= sidx) ? vt - y2 : vt;                                     // H_{t+1}
+            v[t] = (t >= tail) ? vt - y2 : vt;                                   // T_{t+1}
+          }
+          if (sidx == a.n - 1) {                // half complete: every lag gets 2 S2
+            const double s2x2 = 2.0 * m2[h];
+#pragma unroll
+            for (int t = 0; t < T; ++t) v[t] += s2x2;
           }
 #pragma unroll
           for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
-          ring[0] = x;
+          ring[0] = y;
         }
       }
       a.shift[o] = sh[0];

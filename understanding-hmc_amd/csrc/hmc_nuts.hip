@@ -473,9 +473,15 @@ void k_nuts_iters(RandArgs a) {
     // after the second half kick, so that check loads nothing and points l = 3 (mod 4), which
     // check_points only names at m = l + 1, are never saved.
     const bool act = state == S_READY;
-    double dq[M], regB = 0.0;
+    // FAST: dq = q_m - q_{m-1} is dt p_half up to the rounding of q, and the U-turn tests read only
+    // the signs of the dots, so regB = dt (p_half . p_{m-1}) and regA = dt (p_half . p_m) are formed
+    // inside the two half kicks: no dq vector lives across the gradient (56 registers at D = 100).
+    // EXACT keeps the reference's subtraction.
+    constexpr bool DQV = EXACT;
+    const bool dtv = GEN && a.dtv;                      // per-dimension dt: scale each term
+    double dq[DQV ? M : 1], regB = 0.0, regA = 0.0;
 #pragma unroll
-    for (int m = 0; m < M; ++m) dq[m] = 0.0;
+    for (int m = 0; m < (DQV ? M : 1); ++m) dq[m] = 0.0;
     if (act) {
 #pragma unroll
       for (int m = 0; m < M; ++m) {
@@ -485,12 +491,13 @@ void k_nuts_iters(RandArgs a) {
         if constexpr (EXACT) {
           p[m] = p[m] - (dt * (mi * gval<MT>(acc, m))) * 0.5;
           q[m] = q[m] + dt * p[m];
+          dq[m] = q[m] - qk;
+          regB = mac<EXACT>(regB, dq[m], pk);
         } else {
           p[m] = __builtin_fma(-0.5 * dt * mi, gval<MT>(acc, m), p[m]);
           q[m] = __builtin_fma(dt, p[m], q[m]);
+          regB = __builtin_fma(dtv ? dt * p[m] : p[m], pk, regB);
         }
-        dq[m] = q[m] - qk;
-        regB = mac<EXACT>(regB, dq[m], pk);
         if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -502,14 +509,24 @@ void k_nuts_iters(RandArgs a) {
       for (int m = 0; m < M; ++m) {
         const int dd = h + 4 * m;
         const double dt = dim_dt<MT, GEN>(a, dd), mi = dim_minv<MT, GEN>(a, dd);
-        if constexpr (EXACT) p[m] = p[m] - (dt * (mi * gval<MT>(acc, m))) * 0.5;
-        else p[m] = __builtin_fma(-0.5 * dt * mi, gval<MT>(acc, m), p[m]);
+        if constexpr (EXACT) {
+          p[m] = p[m] - (dt * (mi * gval<MT>(acc, m))) * 0.5;
+        } else {
+          const double ph = p[m];
+          p[m] = __builtin_fma(-0.5 * dt * mi, gval<MT>(acc, m), ph);
+          regA = __builtin_fma(dtv ? dt * ph : ph, p[m], regA);
+        }
         if ((m & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
     }
-    double mp1 = 0.0, kp1 = 0.0, regA = 0.0;
+    double mp1 = 0.0, kp1 = 0.0;
+    if constexpr (DQV) {
 #pragma unroll
-    for (int m = 0; m < M; ++m) regA = mac<EXACT>(regA, dq[m], p[m]);
+      for (int m = 0; m < M; ++m) regA = mac<EXACT>(regA, dq[m], p[m]);
+    } else if (!dtv) {
+      regA *= a.dt;
+      regB *= a.dt;
+    }
     if constexpr (MASS) {                               // x.P.x and p.inv(cov_p).p (acc holds the kick)
       double xv[M];
       d4 t[MT];
