@@ -254,7 +254,8 @@ hmc_status hmc_convergence_sums(const double* x, int64_t n_chains, int64_t chain
  * the last `rows` of the carry + rows samples are new.  carry >= min(tmax, pos0) keeps every
  * variogram lag t <= tmax exact.  Accumulates per chain/half/dim shift (first sample), s1 =
  * sum (x - shift), s2 = sum (x - shift)^2 ([n_chains][2][D], zero-initialised) and
- * vsum[t-1][d] += sum over chains of sum (x[p] - x[p-t])^2 for lags t = 1..tmax (tmax in {8,16,32,64}).
+ * vsum[t-1][d] += sum over chains of sum (x[p] - x[p-t])^2 for lags t = 1..tmax (tmax in {8,16,32,64};
+ * a half adds its sums once complete; rows of lags t >= n_half are not variogram sums).
  * Replaces the q_chain-wide passes of utils.py:88-126 and :161-179. */
 int64_t hmc_stream_work_size(int64_t n_chains, int32_t D, int32_t tmax);
 hmc_status hmc_stream_accumulate(const double* window, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,

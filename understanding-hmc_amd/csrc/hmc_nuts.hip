@@ -323,7 +323,13 @@ void k_nuts_iters(RandArgs a) {
       }
       if (__builtin_amdgcn_ballot_w64(state == S_FETCH && live)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the state has reached L2/memory ...
+#ifdef HMC_NUTS_RELACQ
+        // A/B variant: the HIP memory model's own agent-scope release/acquire pair
+        if (state == S_FETCH && live && h == 0)
+          __hip_atomic_store(done + c, (unsigned)(it + 1 - a.it0), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+#else
         if (state == S_FETCH && live && h == 0) st_wt(done + c, (unsigned)(it + 1 - a.it0));   // ... then publish
+#endif
         if (state == S_FETCH) live = false;
       }
       {                                                 // next unit from the queue (converged shuffle)
@@ -346,8 +352,12 @@ void k_nuts_iters(RandArgs a) {
         const unsigned need = (unsigned)(it - a.it0);
         bool ready = need == 0;
         if (!ready) {
+#ifdef HMC_NUTS_RELACQ
+          ready = __hip_atomic_load(done + c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= need;
+#else
           ready = ld_wt(done + c) >= need;
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the state loads below the poll
+#endif
           if (!ready && ++waited > a.wait_cap) {   // broken hand-off: flag it and retire the slot
             ++n_giveup;
             state = S_DONE;
@@ -595,6 +605,67 @@ void k_nuts_iters(RandArgs a) {
     // check points of mpt, incrementally (cp_point): mpt - r + 1, then + r/2, + r/4, ...
     int cp_half = checking ? cp_r(mpt) : 2;
     int cp_pt = mpt - cp_half + 1;
+#ifdef HMC_NUTS_CHECK_PAIRS
+    // A/B variant: two check points per pass (their four vectors in flight together: one memory
+    // round trip per pair); a rejection by either is the reference's outcome (checks have no side
+    // effects, so evaluating the second after a rejecting first changes nothing)
+    for (int ci = 0; ci < ncheck_w; ci += 2) {
+      const bool doit0 = alive_chk && ci < ncheck, doit1 = alive_chk && ci + 1 < ncheck;
+      if (ci > 0) {
+        cp_half >>= 1;
+        cp_pt += cp_half;
+      }
+      const int l0 = doit0 ? cp_pt : 1;
+      const int cp_half1 = cp_half >> 1;
+      const int l1 = doit1 ? cp_pt + cp_half1 : 1;
+      if (ci + 1 < ncheck_w) {
+        cp_half = cp_half1;
+        cp_pt += cp_half1;
+      }
+      const int s0 = save_slot(l0, a.d_max), s1 = save_slot(l1, a.d_max);
+      double r0 = 0.0, l0d = 0.0, r1 = 0.0, l1d = 0.0;
+      if (doit0 || doit1) {
+        double qa[M], pa[M], qb[M], pb[M];
+        if (doit0) {
+          vload<M>(W, V_SLOTS, 2 * s0, qa);
+          vload<M>(W, V_SLOTS + 1, 2 * s0, pa);
+        }
+        if (doit1) {
+          vload<M>(W, V_SLOTS, 2 * s1, qb);
+          vload<M>(W, V_SLOTS + 1, 2 * s1, pb);
+        }
+        double A0 = 0.0, B0 = 0.0, A1 = 0.0, B1 = 0.0;
+        if (doit0) {
+#pragma unroll
+          for (int m = 0; m < M; ++m) {
+            const double Dq = q[m] - qa[m];
+            A0 = mac<EXACT>(A0, Dq, p[m]);
+            B0 = mac<EXACT>(B0, Dq, pa[m]);
+          }
+        }
+        if (doit1) {
+#pragma unroll
+          for (int m = 0; m < M; ++m) {
+            const double Dq = q[m] - qb[m];
+            A1 = mac<EXACT>(A1, Dq, p[m]);
+            B1 = mac<EXACT>(B1, Dq, pb[m]);
+          }
+        }
+        r0 = udir == 0 ? A0 : B0;
+        l0d = udir == 0 ? B0 : A0;
+        r1 = udir == 0 ? A1 : B1;
+        l1d = udir == 0 ? B1 : A1;
+      }
+      r0 = chain_sum4(r0);
+      l0d = chain_sum4(l0d);
+      r1 = chain_sum4(r1);
+      l1d = chain_sum4(l1d);
+      if ((doit0 && l0d < 0.0 && r0 < 0.0) || (doit1 && l1d < 0.0 && r1 < 0.0)) {   // :727-732
+        reject = true;
+        alive_chk = false;
+      }
+    }
+#else
     for (int ci = 0; ci < ncheck_w; ++ci) {
       const bool doit = alive_chk && ci < ncheck;
       if (ci > 0) {
@@ -631,6 +702,7 @@ void k_nuts_iters(RandArgs a) {
         }                                               // (release, :735-736: nothing to free)
       }
     }
+#endif
     NUTS_PHASE(5);
     if (later && !reject) {                             // progressive sampling (:743-751)
       const double E_max_prev = E_max_now;
