@@ -10,6 +10,8 @@
 // Chains are read in place through strides: element (chain m, sample s, dim d) sits at
 //   x[base + m*chain_stride + s*sample_stride + d]
 // which covers q_chain[:, 1:, :], warm-up offsets and thinning without copies.
+#include <type_traits>
+
 #include "hmc_device.hpp"
 #include "hmc_internal.hpp"
 
@@ -306,12 +308,16 @@ struct StreamArgs {
 constexpr int kStreamChunk = 8;   // window rows loaded together (memory-level parallelism)
 
 // Block = 4 chain lanes x 64 dims (lane = dim: coalesced rows).  Each thread walks its chains'
-// new rows once, with the last T shifted samples in a register ring: per element ONE FMA per lag
-// (the product form of k_conv_lags: V_t = 2 S2 - H_t - T_t - 2 C_t; the H_t / T_t terms and the
-// same-half masks only in rows within T of a half's start or end, 2 S2 when a half completes, so
-// vsum holds the variogram sums of every completed half).
+// new rows once, with the last T samples in a register ring.  Two forms of the lag sums:
+//  * PROD (halves of n >= T samples): the product form of k_conv_lags, ONE FMA per lag and row,
+//    V_t = 2 S2 - H_t - T_t - 2 C_t over shifted samples y = x - shift.  The ring is zeroed when a
+//    half starts (so no product crosses halves) and the other terms are three per-half events,
+//    all at static register indices: at position T-1 the ring holds y[T-1..0] (H_t), at n-1 it
+//    holds the half's last T samples (T_t), and 2 S2 is added once the half is complete.  vsum
+//    thus holds the sums of every completed half.
+//  * difference form (short halves): per lag and row (x - x_{-t})^2 under a same-half mask.
 // T <= 16 capped at 168 registers: three waves per SIMD keep enough rows in flight.
-template <int T>
+template <int T, bool PROD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T <= 16 ? 3 : 1))) void k_stream_accum(StreamArgs a) {
   __shared__ double red[4][kDimTile];
   const int dl = threadIdx.x & (kDimTile - 1);
@@ -334,66 +340,104 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T <= 16 ? 3
       double sh[2] = {a.shift[o], a.shift[o + a.D]};
       double m1[2] = {a.s1[o], a.s1[o + a.D]};
       double m2[2] = {a.s2[o], a.s2[o + a.D]};
-      // ring of shifted samples y = x - shift of the first new row's half (carry rows of the other
-      // half are never multiplied: lags are masked to the same half below)
+      // first new row's half and position: carry rows of the same half enter the ring (as y for
+      // PROD), older ones are zero
       const int hc = a.pos0 >= a.n ? 1 : 0;
+      const int sidx0 = (int)(a.pos0 - (int64_t)hc * a.n);
       double ring[T];
 #pragma unroll
-      for (int k = 0; k < T; ++k) ring[k] = (k < a.carry) ? at(a.carry - 1 - k) - sh[hc] : 0.0;
+      for (int k = 0; k < T; ++k) {
+        if constexpr (PROD) ring[k] = (k < a.carry && k < sidx0) ? at(a.carry - 1 - k) - sh[hc] : 0.0;
+        else ring[k] = (k < a.carry) ? at(a.carry - 1 - k) : 0.0;
+      }
       for (int i0 = 0; i0 < rows; i0 += kStreamChunk) {
         double xs[kStreamChunk];
 #pragma unroll
         for (int j = 0; j < kStreamChunk; ++j) xs[j] = (i0 + j < rows) ? at(a.carry + i0 + j) : 0.0;
-        // whole chunk inside one split half with every lag <= T available (uniform over the
-        // block): no same-half selects.  Same operations in the same order as the general path.
-        const int64_t p0 = a.pos0 + i0;
-        const int h0 = p0 >= a.n ? 1 : 0;
-        const int64_t s0 = p0 - (int64_t)h0 * a.n;
-        if (i0 + kStreamChunk <= rows && s0 >= T && s0 + kStreamChunk <= a.n - T) {
+        if constexpr (PROD) {
 #pragma unroll
           for (int j = 0; j < kStreamChunk; ++j) {
-            const double y = xs[j] - sh[h0];
-            m1[h0] += y;
-            m2[h0] = __builtin_fma(y, y, m2[h0]);
-            const double ym2 = -2.0 * y;
+            if (i0 + j < rows) {                  // uniform
+              const int64_t p = a.pos0 + i0 + j;
+              const int h = p >= a.n ? 1 : 0;
+              const int sidx = (int)(p - (int64_t)h * a.n);
+              if (sidx == 0) {                    // a half starts: its shift, an empty ring
+                sh[h] = xs[j];
 #pragma unroll
-            for (int t = 0; t < T; ++t) v[t] = __builtin_fma(ym2, ring[t], v[t]);   // -2 C_t
+                for (int k = 0; k < T; ++k) ring[k] = 0.0;
+              }
+              const double y = xs[j] - sh[h];
+              m1[h] += y;
+              m2[h] = __builtin_fma(y, y, m2[h]);
+              const double ym2 = -2.0 * y;
 #pragma unroll
-            for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
-            ring[0] = y;
+              for (int t = 0; t < T; ++t) v[t] = __builtin_fma(ym2, ring[t], v[t]);   // -2 C_t
+#pragma unroll
+              for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
+              ring[0] = y;
+              if (sidx == T - 1) {                // ring = y[T-1 .. 0]: H_t = sum_{s<t} y^2
+                double q = 0.0;
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                  q = __builtin_fma(ring[T - 1 - t], ring[T - 1 - t], q);
+                  v[t] -= q;
+                }
+              }
+              if (sidx == a.n - 1) {              // ring = the last T samples: T_t; then + 2 S2
+                double q = 0.0;
+                const double s2x2 = 2.0 * m2[h];
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                  q = __builtin_fma(ring[t], ring[t], q);
+                  v[t] += s2x2 - q;
+                }
+              }
+            }
           }
           continue;
         }
-        // rows within T of a half's start or end (rare: not unrolled, the row re-read from cache):
-        // same-half lag masks, the H_t / T_t terms of V_t = 2 S2 - H_t - T_t - 2 C_t, and 2 S2 once
-        // the half is complete (see k_conv_lags)
-#pragma unroll 1
+        // difference form.  Whole chunk inside one split half with every lag <= T available
+        // (uniform over the block): no same-half selects.  Same operations as the general path.
+        const int64_t p0 = a.pos0 + i0;
+        const int h0 = p0 >= a.n ? 1 : 0;
+        const int64_t s0 = p0 - (int64_t)h0 * a.n;
+        if (i0 + kStreamChunk <= rows && s0 >= T && s0 + kStreamChunk <= a.n) {
+#pragma unroll
+          for (int j = 0; j < kStreamChunk; ++j) {
+            const double x = xs[j];
+            const double e = x - sh[h0];
+            m1[h0] += e;
+            m2[h0] = __builtin_fma(e, e, m2[h0]);
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+              const double df = x - ring[t];
+              v[t] = __builtin_fma(df, df, v[t]);
+            }
+#pragma unroll
+            for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
+            ring[0] = x;
+          }
+          continue;
+        }
+#pragma unroll
         for (int j = 0; j < kStreamChunk; ++j) {
           if (i0 + j >= rows) break;
+          const double x = xs[j];
           const int64_t p = a.pos0 + i0 + j;
           const int h = p >= a.n ? 1 : 0;
           const int sidx = (int)(p - (int64_t)h * a.n);
-          const double xj = at(a.carry + i0 + j);
-          if (sidx == 0) sh[h] = xj;
-          const double y = xj - sh[h];
-          m1[h] += y;
-          m2[h] = __builtin_fma(y, y, m2[h]);
-          const double ym2 = -2.0 * y, y2 = y * y;
-          const int tail = a.n - 1 - sidx;      // lags t+1 >= n - sidx count this sample in T_t
+          if (sidx == 0) sh[h] = x;
+          const double e = x - sh[h];
+          m1[h] += e;
+          m2[h] = __builtin_fma(e, e, m2[h]);
 #pragma unroll
           for (int t = 0; t < T; ++t) {
-            double vt = (t < sidx) ? __builtin_fma(ym2, ring[t], v[t]) : v[t];   // lag t+1 inside the half
-            vt = (t >= sidx) ? vt - y2 : vt;                                     // H_{t+1}
-            v[t] = (t >= tail) ? vt - y2 : vt;                                   // T_{t+1}
-          }
-          if (sidx == a.n - 1) {                // half complete: every lag gets 2 S2
-            const double s2x2 = 2.0 * m2[h];
-#pragma unroll
-            for (int t = 0; t < T; ++t) v[t] += s2x2;
+            const double df = x - ring[t];
+            v[t] = (t < sidx) ? __builtin_fma(df, df, v[t]) : v[t];   // lag t+1 inside the same half
           }
 #pragma unroll
           for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
-          ring[0] = y;
+          ring[0] = x;
         }
       }
       a.shift[o] = sh[0];
@@ -492,11 +536,19 @@ hipError_t launch_stream_accum(const double* x, int64_t n_chains, int64_t cs, in
   const int64_t groups = diag_stream_groups(n_chains);
   StreamArgs a{x, n_chains, cs, ss, D, wrap, slot0, carry, rows, n, pos0, shift, s1, s2, vpart, (int)groups};
   dim3 grid((unsigned)groups, (unsigned)((D + kDimTile - 1) / kDimTile));
+  // the product form needs every half to reach position T-1 (its H_t event); both forms give the
+  // same sums of every completed half, and a run keeps one form (n and T are fixed per run)
+  const bool prod = n >= T;
+  auto go = [&](auto t_c) {
+    constexpr int TT = decltype(t_c)::value;
+    if (prod) k_stream_accum<TT, true><<<grid, 256, 0, st>>>(a);
+    else k_stream_accum<TT, false><<<grid, 256, 0, st>>>(a);
+  };
   switch (T) {
-    case 8: k_stream_accum<8><<<grid, 256, 0, st>>>(a); break;
-    case 16: k_stream_accum<16><<<grid, 256, 0, st>>>(a); break;
-    case 32: k_stream_accum<32><<<grid, 256, 0, st>>>(a); break;
-    case 64: k_stream_accum<64><<<grid, 256, 0, st>>>(a); break;
+    case 8: go(std::integral_constant<int, 8>{}); break;
+    case 16: go(std::integral_constant<int, 16>{}); break;
+    case 32: go(std::integral_constant<int, 32>{}); break;
+    case 64: go(std::integral_constant<int, 64>{}); break;
     default: return hipErrorInvalidValue;
   }
   if (hipError_t e = hipGetLastError()) return e;
