@@ -44,13 +44,9 @@ enum : int { S_ITER_START = 0, S_SUB_START = 1, S_READY = 2, S_ITER_END = 3, S_D
 
 // Chain hand-off between slots (any CU, any XCD) inside a launch: the chain's state (q, E_prev, tape
 // cursor) is stored write-through (relaxed agent-scope atomic stores, sc1) and drained
-// (vmcnt(0), at the head of the next wave step) before one lane publishes the chain's iteration
-// count with a relaxed agent-scope store; the taking slot polls that word and reads the state with
-// sc1 loads, issued only once the poll's value is in a register (control dependence), which
-// bypass its CU's L1 (cdna_hip_programming.md Guideline 16, R1).  The HIP memory model's
-// agent-scope release store / acquire load would add an L2 writeback (buffer_wbl2 sc1) per publish
-// and an L2 invalidate (buffer_inv sc1) per poll; measured on the c5 launch (scripts/dev/ab_libs.sh,
-// HMC_NUTS_RELACQ build): 1.761e9 -> 1.667e9 lf/s (-5%), so the sc1 + vmcnt protocol stays.
+// (vmcnt(0)) before one lane publishes the chain's iteration count with a relaxed agent-scope
+// store; the taking slot polls that word and reads the state with sc1 loads, which bypass its
+// CU's L1 (cdna_hip_programming.md Guideline 16, R1).
 template <typename T>
 __device__ __forceinline__ void st_wt(T* p, T x) { __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 template <typename T>
@@ -259,19 +255,8 @@ void k_nuts_iters(RandArgs a) {
   const unsigned long long n_units = (unsigned long long)a.n * (unsigned long long)(a.it1 - a.it0);
   unsigned waited = 0;
   int64_t c = 0;
+  bool live = false;
   uint64_t gc = 0;
-  // The slot's NEXT unit is reserved when a tree starts (res_raw: the queue counter's old value in
-  // lane h = 0, decoded after that step's gradient), and its chain's previous iteration is polled
-  // at the head of later steps (next_ready), so that a tree's end costs ONE memory round trip:
-  // the live point's q (written back) and the next chain's state are loaded together.  The
-  // hand-off word of the finished chain is published one step later (pub: its stores have long
-  // landed by then, so the vmcnt(0) before the publish costs little).
-  unsigned long long res_raw = 0;
-  bool res_pending = false, have_next = false, next_ready = false, pub = false;
-  int64_t cn = 0, pub_c = 0;
-  int itn = 0;
-  unsigned pub_v = 0, poll_v = 0;
-  bool polled = false;
 
   double q[M], p[M];
   d4 acc[MT];
@@ -312,72 +297,42 @@ void k_nuts_iters(RandArgs a) {
   while (true) {
     // ================= transitions (ITER_END -> ITER_START -> SUB_START), converged reductions
     {
-      if (__builtin_amdgcn_ballot_w64(pub)) {          // last step's finished chain: publish
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // its state has reached L2/memory ...
-#ifdef HMC_NUTS_RELACQ
-        // A/B variant: the HIP memory model's own agent-scope release/acquire pair
-        if (pub && h == 0) __hip_atomic_store(done + pub_c, pub_v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-#else
-        if (pub && h == 0) st_wt(done + pub_c, pub_v);  // ... then publish
-#endif
-        pub = false;
-      }
-      polled = have_next && !next_ready && state != S_ITER_END;
-      if (polled) poll_v = ld_wt(done + cn);            // consumed at the end of the step
       const bool at_end = state == S_ITER_END;
       if (at_end) {                                     // samplers.py:786-791: q = live_point_q_old
-        // the finished chain's q (the live point; its gradient is recomputed by whichever slot
-        // takes the chain next, so live points keep no gradient) and, when the next unit's chain
-        // is known to be ready, that chain's state: one round trip for both
-        double qo[M];
-        vload<M>(W, V_OLD_Q, old2, qo);
-        const bool fast = have_next && next_ready;
-        double Enext = 0.0;
-        int64_t tnext = 0;
-        if (fast) {
-#pragma unroll
-          for (int m = 0; m < M; ++m) {
-            const int dd = h + 4 * m;
-            q[m] = dd < a.D ? ld_wt_d(a.q + cn * a.D + dd) : 0.0;
-          }
-          Enext = ld_wt_d(a.Eprev + cn);
-          tnext = REPLAY ? ld_wt(tcur + cn) : 0;
-        }
+        vload<M>(W, V_OLD_Q, old2, q);                  // its gradient: recomputed by the slot that
+                                                        // takes the chain next (S_GRAD), so the live
+                                                        // points keep no gradient vector
         const int qrow = (it - a.wu) / a.thin;
         if (write_row_of(it) && a.qc && qrow >= a.q_row0) {
           double* rowp = a.qc + (c * (int64_t)a.Lq + qrow % a.Lq) * a.D;
 #pragma unroll
           for (int m = 0; m < M; ++m)
-            if (h + 4 * m < a.D) rowp[h + 4 * m] = qo[m];
+            if (h + 4 * m < a.D) rowp[h + 4 * m] = q[m];
         }
-#pragma unroll
-        for (int m = 0; m < M; ++m) {                   // write the chain's state through
-          const int dd = h + 4 * m;
-          if (dd < a.D) st_wt_d(a.q + c * a.D + dd, qo[m]);
-        }
-        if (h == 0) st_wt_d(a.Eprev + c, E_init);
-        if (REPLAY && h == 0) st_wt(tcur + c, tpos);
-        pub = true;                                     // published at the next step's head
-        pub_c = c;
-        pub_v = (unsigned)(it + 1 - a.it0);
-        if (have_next) {
-          c = cn;
-          it = itn;
-          gc = (uint64_t)(a.chain_offset + c);
-          waited = 0;
-          have_next = false;
-          if (fast) {
-            Eprev = Enext;
-            tpos = tnext;
-            state = S_GRAD;                             // gradient at q in this wave step
-          } else {
-            state = S_WAIT;
-          }
-        } else {
-          state = S_DONE;                               // the queue is empty
-        }
+        Eprev = E_init;
+        state = S_FETCH;                                // hand the chain back after each tree
       }
-      {                                                 // first unit of a slot (converged shuffle)
+      if (state == S_FETCH && live) {                   // tree done: write the chain's state through
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          const int dd = h + 4 * m;
+          if (dd < a.D) st_wt_d(a.q + c * a.D + dd, q[m]);
+        }
+        if (h == 0) st_wt_d(a.Eprev + c, Eprev);
+        if (REPLAY && h == 0) st_wt(tcur + c, tpos);
+      }
+      if (__builtin_amdgcn_ballot_w64(state == S_FETCH && live)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the state has reached L2/memory ...
+#ifdef HMC_NUTS_RELACQ
+        // A/B variant: the HIP memory model's own agent-scope release/acquire pair
+        if (state == S_FETCH && live && h == 0)
+          __hip_atomic_store(done + c, (unsigned)(it + 1 - a.it0), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+#else
+        if (state == S_FETCH && live && h == 0) st_wt(done + c, (unsigned)(it + 1 - a.it0));   // ... then publish
+#endif
+        if (state == S_FETCH) live = false;
+      }
+      {                                                 // next unit from the queue (converged shuffle)
         const bool fetching = state == S_FETCH;
         unsigned long long u = (fetching && h == 0) ? atomicAdd(queue, 1ull) : 0ull;
         u = __shfl(u, lane & 15, kWave);
@@ -409,6 +364,7 @@ void k_nuts_iters(RandArgs a) {
           }
         }
         if (ready) {
+          live = true;
 #pragma unroll
           for (int m = 0; m < M; ++m) {
             const int dd = h + 4 * m;
@@ -416,14 +372,12 @@ void k_nuts_iters(RandArgs a) {
           }
           Eprev = ld_wt_d(a.Eprev + c);
           tpos = REPLAY ? ld_wt(tcur + c) : 0;
-          state = S_GRAD;                               // gradient at q in this wave step
+          state = S_GRAD;                               // gradient at q in the next wave step
         }
       }
       const bool starting = state == S_ITER_START;
       double kin = 0.0;
       if (starting) {   // momentum (:565), dims h+4m, streamed to the boundaries: right = p, left = -p (:581-584)
-        if (h == 0) res_raw = atomicAdd(queue, 1ull);   // reserve the slot's next unit now
-        res_pending = true;
         if constexpr (REPLAY) {
           const double* row = a.rp + (c * (int64_t)a.niter + (it - 1)) * a.D;
 #pragma unroll
@@ -559,18 +513,6 @@ void k_nuts_iters(RandArgs a) {
     }
     NUTS_PHASE(1);
     gradient<MT, GEN, true, SHORT>(a, sP, lane, h, q, acc);
-    if (__builtin_amdgcn_ballot_w64(res_pending)) {    // the reservation has landed during the gradient
-      const unsigned long long u = __shfl(res_raw, lane & 15, kWave);
-      if (res_pending) {
-        res_pending = false;
-        have_next = u < n_units;
-        if (have_next) {
-          cn = (int64_t)(u % (unsigned long long)a.n);
-          itn = a.it0 + (int)(u / (unsigned long long)a.n);
-          next_ready = itn == a.it0;                    // a launch's first iteration waits for nothing
-        }
-      }
-    }
     NUTS_PHASE(2);
     if (act) {
 #pragma unroll
@@ -845,19 +787,7 @@ void k_nuts_iters(RandArgs a) {
         state = S_READY;
       }
     }
-    if (polled) {                                       // the poll issued at the head of this step
-      next_ready = poll_v >= (unsigned)(itn - a.it0);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // state loads stay below the poll
-    }
     NUTS_PHASE(7);
-  }
-  if (__builtin_amdgcn_ballot_w64(pub)) {              // chains finished in the last step
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifdef HMC_NUTS_RELACQ
-    if (pub && h == 0) __hip_atomic_store(done + pub_c, pub_v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-#else
-    if (pub && h == 0) st_wt(done + pub_c, pub_v);
-#endif
   }
 #ifdef HMC_DEBUG_HOOKS
   if (a.stamps && lane == 0) {
