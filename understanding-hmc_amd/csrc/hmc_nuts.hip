@@ -46,7 +46,13 @@ enum : int { S_ITER_START = 0, S_SUB_START = 1, S_READY = 2, S_ITER_END = 3, S_D
 // cursor) is stored write-through (relaxed agent-scope atomic stores, sc1) and drained
 // (vmcnt(0)) before one lane publishes the chain's iteration count with a relaxed agent-scope
 // store; the taking slot polls that word and reads the state with sc1 loads, which bypass its
-// CU's L1 (cdna_hip_programming.md Guideline 16, R1).
+// CU's L1 (cdna_hip_programming.md Guideline 16, R1).  The HIP memory model's agent-scope release
+// store / acquire load would add an L2 writeback (buffer_wbl2 sc1) per publish and an L2
+// invalidate (buffer_inv sc1) per poll; measured on the c5 launch (scripts/dev/ab_libs.sh,
+// HMC_NUTS_RELACQ build): 1.761e9 -> 1.667e9 lf/s (-5%), so the sc1 + vmcnt protocol stays.
+// Reserving the next unit at tree start and polling its chain during the tree (so that a tree's
+// end costs one round trip) measured 1.77e9 -> 1.52e9 lf/s: those loads sit in the in-order vmcnt
+// queue ahead of the U-turn checks' loads, which then wait for them.
 template <typename T>
 __device__ __forceinline__ void st_wt(T* p, T x) { __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 template <typename T>
