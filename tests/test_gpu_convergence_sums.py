@@ -1,0 +1,71 @@
+"""hmc_convergence_sums (the one-pass R-hat / variogram sums behind convergence_stats,
+utils.py:77-179) against a float64 NumPy restatement of the same sums, over the shapes both
+lag kernels meet: the direct-to-LDS kernel (even D, 16-B aligned rows) and the register-staged
+one (odd D, odd strides, a misaligned view), n below / at / above the chunk and lag widths, one
+or few split chains per block group, and every lag width tmax in {8, 16, 32, 64}.
+
+The sums are the ones include/hmc.h documents: rows [sum_j std_j, sum_j (mean_j - S),
+sum_j (mean_j - S)^2, V_1 .. V_tmax] with S = the view's first sample and
+V_t = sum_j sum_{s < n-t} (x_j[s+t] - x_j[s])^2 (0 for t >= n)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _expected(view, n, tmax):
+    """view: (Nchain, >= 2n, D) float64 NumPy; split chain 2m+h = view[m, h n : (h+1) n]."""
+    N, _, D = view.shape
+    xs = np.concatenate([view[:, :n], view[:, n:2 * n]], axis=0)      # (2N, n, D)
+    S = view[0, 0]
+    mean = xs.mean(axis=1)
+    std = xs.std(axis=1, ddof=1)
+    out = np.zeros((3 + tmax, D))
+    out[0] = std.sum(axis=0)
+    out[1] = (mean - S).sum(axis=0)
+    out[2] = ((mean - S) ** 2).sum(axis=0)
+    for t in range(1, min(tmax, n - 1) + 1):
+        out[2 + t] = ((xs[:, t:] - xs[:, :-t]) ** 2).sum(axis=(0, 1))
+    return out
+
+
+CASES = [
+    # (Nchain, Niter, Dtot, dim slice start, thin, warm-up, tmax)
+    (37, 201, 100, 0, 1, 1, 64),       # LDS kernel: headline D, n = 100
+    (5, 41, 100, 0, 1, 1, 16),         # n = 20: one full chunk + a ragged one
+    (3, 9, 64, 0, 1, 1, 8),            # n = 4 < TW
+    (64, 67, 130, 0, 1, 3, 32),        # n = 32 = T; 3 dim tiles, a ragged last one
+    (2, 260, 2, 0, 1, 0, 64),          # D = 2: one dim pair; n = 130 > tmax
+    (1000, 34, 100, 0, 1, 0, 16),      # many split chains per block group, n = 17
+    (9, 300, 101, 0, 3, 2, 64),        # odd D -> register-staged kernel, thinned view
+    (9, 300, 101, 1, 1, 1, 64),        # D = 100 view, odd row stride -> register-staged kernel
+    (9, 300, 100, -1, 1, 1, 64),       # even strides, storage at an 8-B offset -> register-staged
+    (11, 120, 100, 0, 3, 0, 32),       # even stride x thin: LDS kernel on a thinned view
+]
+
+
+@pytest.mark.parametrize("N,Niter,Dtot,d0,thin,wu,tmax", CASES)
+def test_convergence_sums_vs_numpy(N, Niter, Dtot, d0, thin, wu, tmax):
+    from hmc_amd.diagnostics import _Split, convergence_sums
+
+    rng = np.random.default_rng(N * 1000 + Niter + Dtot + tmax)
+    # AR(1) chains around a per-dim offset, so that lags carry structure and shifts matter
+    q = np.empty((N, Niter, Dtot))
+    q[:, 0] = rng.normal(size=(N, Dtot))
+    for t in range(1, Niter):
+        q[:, t] = 0.8 * q[:, t - 1] + rng.normal(size=(N, Dtot))
+    q += rng.normal(size=Dtot) * 5.0
+    if d0 >= 0:
+        t_dev = torch.as_tensor(q).cuda()[:, :, d0:]
+    else:                              # the same array one double into its storage (8-B aligned only)
+        flat = torch.zeros(q.size + 1, dtype=torch.float64, device="cuda")
+        flat[1:] = torch.as_tensor(q.reshape(-1)).cuda()
+        t_dev = flat[1:].view(q.shape)
+        assert t_dev.data_ptr() % 16 == 8
+        d0 = 0
+    sp = _Split(t_dev, thin, wu)
+    got = convergence_sums(sp, tmax).cpu().numpy()
+    view = q[:, wu::thin, d0:]
+    want = _expected(view, sp.n, tmax)
+    np.testing.assert_allclose(got, want, rtol=1e-10, atol=1e-9 * np.abs(want).max())

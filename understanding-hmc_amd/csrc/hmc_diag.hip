@@ -287,6 +287,142 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   }
 }
 
+// The same sums with the series staged through LDS: each block runs SL = 4/G split chains at a time
+// (G waves each, one per lag group, as k_conv_lags) through a per-slot LDS ring of rows (lane = dim).
+// The G waves of a slot bring the slot's next rows in with direct-to-LDS loads
+// (global_load_lds_dwordx4: 16 B per lane, two 512-B rows per wave-instruction, no registers),
+// PD chunks of TW rows ahead, and every wave reads its current row and its delayed row (gTW back)
+// from the ring: one HBM read per element, no load buffers in registers, and the loads of PD
+// chunks in flight behind the lag products (the register-staged k_conv_lags is latency-bound).
+template <int TW, int G, int PD>
+__global__ __launch_bounds__(256) void k_conv_lds(Src s, int groups, int ntiles, double* partial) {
+  constexpr int SL = 4 / G;                       // split chains per block at a time
+  constexpr int T = TW * G;
+  constexpr int RB = (G + PD) * TW;               // ring rows per slot (multiple of TW)
+  constexpr int NI = TW / 2 / G;                  // DMA instructions per wave and chunk (2 rows each)
+  static_assert(NI >= 1 && NI * 2 * G == TW, "TW must be a multiple of 2G");
+  __shared__ double ring_x[SL * RB * kDimTile];
+  __shared__ double red[4][kDimTile];
+  const int lane = threadIdx.x & (kDimTile - 1);
+  const int dl = lane;
+  const int w = threadIdx.x / kDimTile;
+  const int slot = w / G, g = w % G;
+  const int gofs = g * TW;
+  const int b = blockIdx.x;                       // XCD-aware: tiles of a group 8 blocks apart
+  const int tile = (b >> 3) % ntiles;
+  const int grp = (b & 7) + 8 * ((b >> 3) / ntiles);
+  const int d = tile * kDimTile + dl;
+  const int64_t m2 = 2 * s.n_chains;
+  const int n = s.n;
+  const int nch = (n + TW - 1) / TW;              // chunks per split chain
+  const int64_t stride = (int64_t)groups * SL;
+  const int64_t j0 = (int64_t)grp * SL;
+  const int K = grp < groups ? (int)((m2 - j0 + stride - 1) / stride) : 0;   // split chains per slot (max)
+  const int F = K * nch;                          // (split chain, chunk) items, the same for all slots
+  double* const my = ring_x + slot * RB * kDimTile;
+  // DMA of item f into ring rows (f TW) % RB ...: wave g moves rows 2(g + G e), +1 of the chunk
+  const int drow = lane >> 5, dcol = (lane & 31) * 2;   // this lane's row (of 2) and dim pair
+  auto issue = [&](int f) {
+    const int64_t j = j0 + slot + (int64_t)(f / nch) * stride;
+    const int cc = f % nch;
+    const int r0 = (f * TW) % RB;
+#pragma unroll
+    for (int e = 0; e < NI; ++e) {
+      const int rr = 2 * (g + G * e);             // row pair inside the chunk
+      const int row = cc * TW + rr + drow;
+      const bool ok = j < m2 && row < n && tile * kDimTile + dcol < s.D;   // D even: whole pairs
+      const double* src = ok ? split_ptr(s, j, row) + tile * kDimTile + dcol : s.x + s.base;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(my + (r0 + rr) * kDimTile),
+                                       16, 0, 0);
+    }
+  };
+  double v[TW];
+#pragma unroll
+  for (int k = 0; k < TW; ++k) v[k] = 0.0;
+  double a_std = 0.0, a_m = 0.0, a_m2 = 0.0;
+  const double S = d < s.D ? s.x[s.base + d] : 0.0;
+  double ring[TW];
+  double sh = 0.0, s1 = 0.0, s2 = 0.0, r1 = 0.0, sufb = 0.0;
+  const int pos_suf = n - gofs - 1;
+  for (int f = 0; f < PD && f < F; ++f) issue(f);
+  for (int f = 0; f < F; ++f) {
+    // item f's rows have landed (PD - 1 newer items may still fly), and every wave is past item f-1
+    if (f + PD - 1 < F) {
+      if constexpr (PD == 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NI) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (f + PD < F) issue(f + PD);
+    const int64_t j = j0 + slot + (int64_t)(f / nch) * stride;
+    const int cc = f % nch;
+    const int rc = (f * TW) % RB;                 // ring row of this chunk's first row
+    const int rd = (rc - gofs + RB) % RB;         // ... of the delayed stream's
+    if (j < m2 && d < s.D) {
+      if (cc == 0) {                              // a split chain starts
+        sh = my[rc * kDimTile + dl];
+#pragma unroll
+        for (int k = 0; k < TW; ++k) ring[k] = 0.0;
+        s1 = s2 = r1 = sufb = 0.0;
+      }
+      const bool hwin = cc * TW == gofs;          // this chunk's running S2 gives H_t of our lags
+#pragma unroll
+      for (int i = 0; i < TW; ++i) {
+        const int sp = cc * TW + i;
+        if (sp < n) {
+          const double x = my[(rc + i) * kDimTile + dl];
+          const double xd = sp >= gofs ? my[(rd + i) * kDimTile + dl] : sh;
+          r1 += x;
+          const double y = x - sh;
+          s1 += y;
+          s2 = __builtin_fma(y, y, s2);
+          const double ym2 = -2.0 * y;
+#pragma unroll
+          for (int k = 0; k < TW; ++k) v[k] = __builtin_fma(ym2, ring[k], v[k]);
+          if (hwin) v[i] -= s2;
+          if (sp == pos_suf) sufb = s2;
+#pragma unroll
+          for (int k = TW - 1; k > 0; --k) ring[k] = ring[k - 1];
+          ring[0] = xd - sh;
+        }
+      }
+      if (cc == nch - 1) {                        // the split chain is complete
+        double q = pos_suf >= 0 ? s2 - sufb : s2;
+        const double s2x2 = 2.0 * s2;
+#pragma unroll
+        for (int k = 0; k < TW; ++k) {
+          q = __builtin_fma(ring[k], ring[k], q);
+          v[k] += s2x2 - q;
+        }
+        const double mean = r1 / n;
+        const double dm = mean - sh;
+        const double mm2 = (s2 - 2.0 * dm * s1) + n * (dm * dm);
+        a_std += sqrt(mm2 > 0.0 ? mm2 / (n - 1) : 0.0);
+        const double e = mean - S;
+        a_m += e;
+        a_m2 = __builtin_fma(e, e, a_m2);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  auto put = [&](int row, double x) {
+    red[w][dl] = x;
+    __syncthreads();
+    if (w == 0 && d < s.D && grp < groups)
+      partial[((int64_t)grp * (T + 3) + row) * s.D + d] = ((red[0][dl] + red[1][dl]) + red[2][dl]) + red[3][dl];
+    __syncthreads();
+  };
+  put(0, g == 0 ? a_std : 0.0);
+  put(1, g == 0 ? a_m : 0.0);
+  put(2, g == 0 ? a_m2 : 0.0);
+#pragma unroll
+  for (int gg = 0; gg < G; ++gg) {
+#pragma unroll
+    for (int k = 0; k < TW; ++k) put(3 + gg * TW + k, g == gg ? v[k] : 0.0);
+  }
+}
+
 // ---- streaming (windowed) split-chain statistics: q_chain never has to be stored whole.
 // Sample position p (0-based over q_chain[:, 1:, :]) lies in split half h = p / n at offset
 // s = p - h*n (positions >= 2n are not part of any split chain, utils.py:102-104).  A call
@@ -460,9 +596,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T <= 16 ? 3
 
 int64_t rows_chunks(int64_t rows) { return (rows + kRowChunk - 1) / kRowChunk; }
 
-int64_t conv_groups(int64_t n_chains) {
+// Blocks resident per CU for the lag kernel of T lags (LDS ring and VGPRs; see the launch switch).
+constexpr int conv_blocks_per_cu(int T) { return T == 16 ? 1 : T == 32 ? 2 : 3; }
+
+// Block groups of the lag pass: one resident wave of blocks over all dim tiles (no tail wave).
+int64_t conv_groups(int64_t n_chains, int D, int T) {
   const int64_t g = (2 * n_chains + 3) / 4;       // 4 split chains per block row set
-  const int64_t cap = 512;                        // ~2 resident blocks per CU per dim tile
+  const int ntiles = (D + kDimTile - 1) / kDimTile;
+  int64_t cap = (int64_t)256 * conv_blocks_per_cu(T) / ntiles;
+  cap = cap >= 8 ? cap / 8 * 8 : 8;
   return g < cap ? (g < 1 ? 1 : g) : cap;
 }
 
@@ -502,21 +644,30 @@ hipError_t launch_rowsum(const double* x, int64_t n_outer, int64_t os, int64_t n
   return hipGetLastError();
 }
 
-int64_t diag_conv_work(int64_t n_chains, int D, int T) { return conv_groups(n_chains) * (int64_t)(T + 3) * D; }
+int64_t diag_conv_work(int64_t n_chains, int D, int T) { return conv_groups(n_chains, D, T) * (int64_t)(T + 3) * D; }
 
 hipError_t launch_conv_fused(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int64_t base, int n, int D,
                              int T, double* work, double* out, hipStream_t st) {
   Src s{x, cs, ss, base, n_chains, n, D};
-  const int64_t groups = conv_groups(n_chains);
+  const int64_t groups = conv_groups(n_chains, D, T);
   const int ntiles = (D + kDimTile - 1) / kDimTile;
   // blocks: 8 groups x ntiles per 8 * ntiles consecutive block ids (XCD-aware order, see kernel)
   const int64_t gpad = (groups + 7) / 8 * 8;
   const dim3 grid((unsigned)(gpad * ntiles));
-  switch (T) {   // T = TW x G lags
-    case 8: k_conv_lags<8, 1><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
-    case 16: k_conv_lags<16, 1><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
-    case 32: k_conv_lags<16, 2><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
-    case 64: k_conv_lags<16, 4><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
+  // the direct-to-LDS loads move dim pairs of 16 B: rows must start 16-B aligned and hold whole pairs
+  if (((D | cs | ss | base) & 1) || (reinterpret_cast<uintptr_t>(x) & 15)) {
+    switch (T) {
+      case 8: k_conv_lags<8, 1><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
+      case 16: k_conv_lags<16, 1><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
+      case 32: k_conv_lags<16, 2><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
+      case 64: k_conv_lags<16, 4><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else switch (T) {   // T = TW x G lags; rows staged through LDS by direct-to-LDS loads, 2 chunks ahead
+    case 8: k_conv_lds<8, 1, 2><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
+    case 16: k_conv_lds<16, 1, 2><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
+    case 32: k_conv_lds<16, 2, 2><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
+    case 64: k_conv_lds<16, 4, 2><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
     default: return hipErrorInvalidValue;
   }
   if (hipError_t e = hipGetLastError()) return e;
