@@ -37,15 +37,23 @@ L = H.lib()
 L.hmc_debug_stamps.restype = ctypes.c_int64
 L.hmc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
 waves = min((N + 63) // 64, torch.cuda.get_device_properties(0).multi_processor_count) * 4
-buf = np.zeros(waves * 8, dtype=np.uint64)
+W = 16                                             # kStampWords (hmc_internal.hpp)
+buf = np.zeros(waves * W, dtype=np.uint64)
 got = L.hmc_debug_stamps(buf.ctypes.data, buf.size)
-ph = buf[:got].reshape(-1, 8).astype(np.float64)
-tot = ph.sum(axis=0)
+ph = buf[:got].reshape(-1, W).astype(np.float64)
+tot = ph[:, :8].sum(axis=0)
+sub = ph[:, 8:13].sum(axis=0)
+end_steps = ph[:, 13].sum()
 names = ["transitions", "kick+drift", "gradient (MFMA)", "kick+energies", "new point / saves",
          "loaded U-turn checks", "progressive sampling", "sub-tree end"]
+sub_names = ["tree end (live point, row)", "write-back + drain + publish", "queue reservation",
+             "poll + state loads", "momentum + tree start"]
 steps = int(c[H.CNT_LEAPFROG_SQ])
 out = dict(N=N, S=S, D=D, rho=rho, launch_ms=ms, leapfrogs=int(c[H.CNT_LEAPFROG]), wave_steps=steps,
            lane_utilisation=float(c[H.CNT_LEAPFROG]) / (16 * steps), lf_per_s=float(c[H.CNT_LEAPFROG]) / (ms / 1e3),
            waves=waves, phase_fraction={n: float(t / tot.sum()) for n, t in zip(names, tot)},
-           phase_clk_per_step={n: float(t / max(steps, 1) * waves / max(waves, 1)) for n, t in zip(names, tot)})
+           phase_clk_per_step={n: float(t / max(steps, 1)) for n, t in zip(names, tot)},
+           steps_with_tree_end=float(end_steps / max(steps, 1)),
+           transition_clk_per_step={n: float(t / max(steps, 1)) for n, t in zip(sub_names, sub)},
+           transition_clk_per_tree_end_step={n: float(t / max(end_steps, 1)) for n, t in zip(sub_names, sub)})
 print(json.dumps(out, indent=1))

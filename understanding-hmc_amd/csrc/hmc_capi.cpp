@@ -138,7 +138,7 @@ hmc::RandArgs rand_args(const hmc_target* t, const hmc_kinetic* k, const hmc_sch
     if (g_stamps) (void)hipFree(g_stamps);
     g_stamps = nullptr;
     g_stamp_waves = waves;
-    if (hipMalloc(&g_stamps, waves * 8 * sizeof(unsigned long long)) == hipSuccess) a.stamps = g_stamps;
+    if (hipMalloc(&g_stamps, waves * hmc::kStampWords * sizeof(unsigned long long)) == hipSuccess) a.stamps = g_stamps;
   }
 #endif
   if (st->traj_q && st->traj_len && st->decision && st->n_save > 0) {
@@ -163,7 +163,7 @@ extern "C" {
 // Diagnostic: copy the per-wave phase timers of the last HMC_DEBUG_STAMPS launch (debug build only).
 int64_t hmc_debug_stamps(unsigned long long* host, int64_t cap_words) {
   if (!g_stamps) return 0;
-  const int64_t words = g_stamp_waves * 8 < cap_words ? g_stamp_waves * 8 : cap_words;
+  const int64_t words = g_stamp_waves * hmc::kStampWords < cap_words ? g_stamp_waves * hmc::kStampWords : cap_words;
   if (hipDeviceSynchronize() != hipSuccess) return 0;
   if (hipMemcpy(host, g_stamps, words * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return 0;
   return words;

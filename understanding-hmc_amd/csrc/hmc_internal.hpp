@@ -7,6 +7,8 @@
 
 namespace hmc {
 
+constexpr int kStampWords = 16;   // debug phase-timer words per wave (HMC_DEBUG_STAMPS)
+
 // Lane-group layout of one chain inside a wave64 (see hmc_device.hpp).
 struct Layout {
   int K;       // coordinate pairs per lane
@@ -54,7 +56,8 @@ struct RandArgs {
   int64_t tape_stride;
   int dbg;               // ablation flags (HMC_DEBUG_ABLATE env; 0 in normal runs)
   int dbgL;              // forced trajectory length (HMC_DEBUG_L env; -1 in normal runs)
-  unsigned long long* stamps;  // diagnostic phase timers (HMC_DEBUG_STAMPS env; null in normal runs)
+  unsigned long long* stamps;  // diagnostic phase timers (HMC_DEBUG_STAMPS env; null in normal runs),
+                               // kStampWords per wave
   const int32_t* order;  // dense: tile slot -> chain (L-ordered tiles) or null (slot = chain)
   double* gcache;        // dense: per-chain gradient at q [n][D] (in the order workspace) or null
   const int32_t* gvalid; // dense: nonzero once gcache holds the gradient of every chain's q

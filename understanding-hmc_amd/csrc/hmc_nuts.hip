@@ -90,7 +90,9 @@ __device__ __forceinline__ int nuts_nvec(int d_max) { return V_SLOTS + 2 * (d_ma
 // Phase timers of the debug build (make debug; HMC_DEBUG_STAMPS): wave-uniform s_memtime deltas per
 // part of a wave step, summed over the launch: 0 transitions, 1 half kick + drift, 2 gradient
 // (MFMA), 3 half kick + energies, 4 new-point bookkeeping / saves, 5 loaded U-turn checks,
-// 6 progressive sampling, 7 sub-tree end.  The release library compiles none of it.
+// 6 progressive sampling, 7 sub-tree end; inside 0: 8 tree end (live point, row), 9 write-back +
+// drain + publish, 10 queue reservation, 11 poll + state loads, 12 momentum + tree start; 13 counts
+// the wave steps with a tree end.  The release library compiles none of it.
 #ifdef HMC_DEBUG_HOOKS
 #define NUTS_PHASE(i)                                        \
   do {                                                       \
@@ -101,6 +103,18 @@ __device__ __forceinline__ int nuts_nvec(int d_max) { return V_SLOTS + 2 * (d_ma
 #else
 #define NUTS_PHASE(i) \
   do {                \
+  } while (0)
+#endif
+#ifdef HMC_DEBUG_HOOKS
+#define NUTS_SUBPHASE(i)                                     \
+  do {                                                       \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    ph[i] += t_ - t_sub;                                     \
+    t_sub = t_;                                              \
+  } while (0)
+#else
+#define NUTS_SUBPHASE(i) \
+  do {                   \
   } while (0)
 #endif
 
@@ -282,8 +296,8 @@ void k_nuts_iters(RandArgs a) {
   int old2 = 0;                                         // vector offset of the live_point_old pair
   unsigned long long n_lf = 0, n_unst = 0, n_dmax = 0, n_tape = 0, n_steps = 0, n_giveup = 0;
 #ifdef HMC_DEBUG_HOOKS
-  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long t_ph = __builtin_amdgcn_s_memtime();
+  unsigned long long ph[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_ph = __builtin_amdgcn_s_memtime(), t_sub = t_ph;
 #endif
 
   auto draw = [&](bool direction) -> double {           // next random number of this chain (reference order)
@@ -304,6 +318,10 @@ void k_nuts_iters(RandArgs a) {
     // ================= transitions (ITER_END -> ITER_START -> SUB_START), converged reductions
     {
       const bool at_end = state == S_ITER_END;
+#ifdef HMC_DEBUG_HOOKS
+      t_sub = __builtin_amdgcn_s_memtime();
+      if (__builtin_amdgcn_ballot_w64(at_end)) ++ph[13];
+#endif
       if (at_end) {                                     // samplers.py:786-791: q = live_point_q_old
         vload<M>(W, V_OLD_Q, old2, q);                  // its gradient: recomputed by the slot that
                                                         // takes the chain next (S_GRAD), so the live
@@ -318,6 +336,7 @@ void k_nuts_iters(RandArgs a) {
         Eprev = E_init;
         state = S_FETCH;                                // hand the chain back after each tree
       }
+      NUTS_SUBPHASE(8);
       if (state == S_FETCH && live) {                   // tree done: write the chain's state through
 #pragma unroll
         for (int m = 0; m < M; ++m) {
@@ -338,6 +357,7 @@ void k_nuts_iters(RandArgs a) {
 #endif
         if (state == S_FETCH) live = false;
       }
+      NUTS_SUBPHASE(9);
       {                                                 // next unit from the queue (converged shuffle)
         const bool fetching = state == S_FETCH;
         unsigned long long u = (fetching && h == 0) ? atomicAdd(queue, 1ull) : 0ull;
@@ -354,6 +374,7 @@ void k_nuts_iters(RandArgs a) {
           }
         }
       }
+      NUTS_SUBPHASE(10);
       if (state == S_WAIT) {                            // the chain's previous iteration published?
         const unsigned need = (unsigned)(it - a.it0);
         bool ready = need == 0;
@@ -381,6 +402,7 @@ void k_nuts_iters(RandArgs a) {
           state = S_GRAD;                               // gradient at q in the next wave step
         }
       }
+      NUTS_SUBPHASE(11);
       const bool starting = state == S_ITER_START;
       double kin = 0.0;
       if (starting) {   // momentum (:565), dims h+4m, streamed to the boundaries: right = p, left = -p (:581-584)
@@ -476,6 +498,7 @@ void k_nuts_iters(RandArgs a) {
         k = 0;
         state = S_READY;
       }
+      NUTS_SUBPHASE(12);
     }
     if (!__builtin_amdgcn_ballot_w64(state != S_DONE)) break;
     NUTS_PHASE(0);
@@ -798,7 +821,7 @@ void k_nuts_iters(RandArgs a) {
 #ifdef HMC_DEBUG_HOOKS
   if (a.stamps && lane == 0) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) a.stamps[wv * 8 + i] = ph[i];
+    for (int i = 0; i < 14; ++i) a.stamps[wv * kStampWords + i] = ph[i];
   }
 #endif
 

@@ -317,14 +317,14 @@ __global__ __launch_bounds__(256) void k_random_iters(RandArgs a) {
   if (a.stamps && ln.lane == 0) {
     const int64_t wv = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) a.stamps[wv * 8 + i] = ph[i];
-    a.stamps[wv * 8 + 6] = t_start;
-    a.stamps[wv * 8 + 7] = stamp(true);
+    for (int i = 0; i < 6; ++i) a.stamps[wv * kStampWords + i] = ph[i];
+    a.stamps[wv * kStampWords + 6] = t_start;
+    a.stamps[wv * kStampWords + 7] = stamp(true);
     // hardware placement: HW_ID (wave/simd/cu/sh/se) in the high word of slot 5's neighbour
     const unsigned hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
     const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
-    a.stamps[wv * 8 + 5] = ((unsigned long long)hwid << 32) | ((unsigned long long)(xcc & 0xffff) << 16) |
-                           (a.stamps[wv * 8 + 5] & 0xffffull);
+    a.stamps[wv * kStampWords + 5] = ((unsigned long long)hwid << 32) | ((unsigned long long)(xcc & 0xffff) << 16) |
+                           (a.stamps[wv * kStampWords + 5] & 0xffffull);
   }
   n_acc = wave_sum_u64(n_acc);
   n_acc_wu = wave_sum_u64(n_acc_wu);
