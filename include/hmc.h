@@ -238,7 +238,7 @@ hmc_status hmc_variogram(const double* x, int64_t n_chains, int64_t chain_stride
  *   row 0        sum_j std_j (ddof=1)                       (W, utils.py:109-112)
  *   row 1        sum_j (mean_j - S_d)                       (mean_all, :116-119)
  *   row 2        sum_j (mean_j - S_d)^2                     (B, :120, after re-centring)
- *   row 2 + t    sum_j sum_s (x_j[s+t] - x_j[s])^2, t = 1..tmax (variogram, :161-179; valid for t < n)
+ *   row 2 + t    sum_j sum_s (x_j[s+t] - x_j[s])^2, t = 1..tmax (variogram, :161-179; 0 for t >= n)
  * over the 2*n_chains split chains j (same strided view as hmc_split_moments), S_d = x[base + d]
  * (the view's first sample: a common shift so that B needs no second pass).  tmax in
  * {8, 16, 32, 64}; longer lags: hmc_variogram.  Deterministic (fixed-order two-stage sums). */

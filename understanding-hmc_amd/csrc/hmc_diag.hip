@@ -283,7 +283,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
   for (int gg = 0; gg < G; ++gg) {
 #pragma unroll
-    for (int k = 0; k < TW; ++k) put(3 + gg * TW + k, g == gg ? v[k] : 0.0);
+    for (int k = 0; k < TW; ++k) put(3 + gg * TW + k, g == gg && gg * TW + k + 1 < s.n ? v[k] : 0.0);   // lags t >= n: 0
   }
 }
 
@@ -419,7 +419,7 @@ __global__ __launch_bounds__(256) void k_conv_lds(Src s, int groups, int ntiles,
 #pragma unroll
   for (int gg = 0; gg < G; ++gg) {
 #pragma unroll
-    for (int k = 0; k < TW; ++k) put(3 + gg * TW + k, g == gg ? v[k] : 0.0);
+    for (int k = 0; k < TW; ++k) put(3 + gg * TW + k, g == gg && gg * TW + k + 1 < s.n ? v[k] : 0.0);   // lags t >= n: 0
   }
 }
 
