@@ -11,6 +11,7 @@
 //   x[base + m*chain_stride + s*sample_stride + d]
 // which covers q_chain[:, 1:, :], warm-up offsets and thinning without copies.
 #include <type_traits>
+#include <utility>
 
 #include "hmc_device.hpp"
 #include "hmc_internal.hpp"
@@ -294,8 +295,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 // PD chunks of TW rows ahead, and every wave reads its current row and its delayed row (gTW back)
 // from the ring: one HBM read per element, no load buffers in registers, and the loads of PD
 // chunks in flight behind the lag products (the register-staged k_conv_lags is latency-bound).
+// f(std::integral_constant<int, r>) for the runtime r in [0, N): a uniform branch to one of N
+// statically indexed bodies
+template <class F, int... I>
+__device__ __forceinline__ void static_dispatch_(int r, F& f, std::integer_sequence<int, I...>) {
+  ((r == I ? f(std::integral_constant<int, I>{}) : void()), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_dispatch(int r, F& f) {
+  static_dispatch_(r, f, std::make_integer_sequence<int, N>{});
+}
+
 template <int TW, int G, int PD>
-__global__ __launch_bounds__(256) void k_conv_lds(Src s, int groups, int ntiles, double* partial) {
+__global__ __launch_bounds__(256, 3) void k_conv_lds(Src s, int groups, int ntiles, double* partial) {
   constexpr int SL = 4 / G;                       // split chains per block at a time
   constexpr int T = TW * G;
   constexpr int RB = (G + PD) * TW;               // ring rows per slot (multiple of TW)
@@ -366,35 +378,50 @@ __global__ __launch_bounds__(256) void k_conv_lds(Src s, int groups, int ntiles,
         for (int k = 0; k < TW; ++k) ring[k] = 0.0;
         s1 = s2 = r1 = sufb = 0.0;
       }
+      // ring slot i holds the delayed value of chunk row i (the chunks are TW-aligned), so at row i
+      // lag gofs + 1 + k reads slot (i - 1 - k) mod TW: static registers, no ring shifts
+      const int rem = n - cc * TW;                // rows of this chunk
       const bool hwin = cc * TW == gofs;          // this chunk's running S2 gives H_t of our lags
+      const bool dly = cc * TW >= gofs;           // the delayed rows exist (gofs is a multiple of TW)
+      const int isuf = pos_suf - cc * TW;         // suffix mark (T_t terms), if inside this chunk
+      auto rows = [&](auto plain_c) {
+        constexpr bool PLAIN = decltype(plain_c)::value;   // whole chunk, no H_t / suffix event
 #pragma unroll
-      for (int i = 0; i < TW; ++i) {
-        const int sp = cc * TW + i;
-        if (sp < n) {
-          const double x = my[(rc + i) * kDimTile + dl];
-          const double xd = sp >= gofs ? my[(rd + i) * kDimTile + dl] : sh;
-          r1 += x;
-          const double y = x - sh;
-          s1 += y;
-          s2 = __builtin_fma(y, y, s2);
-          const double ym2 = -2.0 * y;
+        for (int i = 0; i < TW; ++i) {
+          if (PLAIN || i < rem) {
+            const double x = my[(rc + i) * kDimTile + dl];
+            const double xd = dly ? my[(rd + i) * kDimTile + dl] : sh;
+            r1 += x;
+            const double y = x - sh;
+            s1 += y;
+            s2 = __builtin_fma(y, y, s2);
+            const double ym2 = -2.0 * y;
 #pragma unroll
-          for (int k = 0; k < TW; ++k) v[k] = __builtin_fma(ym2, ring[k], v[k]);
-          if (hwin) v[i] -= s2;
-          if (sp == pos_suf) sufb = s2;
-#pragma unroll
-          for (int k = TW - 1; k > 0; --k) ring[k] = ring[k - 1];
-          ring[0] = xd - sh;
+            for (int k = 0; k < TW; ++k) v[k] = __builtin_fma(ym2, ring[(i - 1 - k) & (TW - 1)], v[k]);
+            if (!PLAIN) {
+              if (hwin) v[i] -= s2;
+              if (i == isuf) sufb = s2;
+            }
+            ring[i] = xd - sh;
+          }
         }
-      }
+      };
+      if (rem >= TW && !hwin && (isuf < 0 || isuf >= TW)) rows(std::true_type{});
+      else rows(std::false_type{});
       if (cc == nch - 1) {                        // the split chain is complete
         double q = pos_suf >= 0 ? s2 - sufb : s2;
         const double s2x2 = 2.0 * s2;
+        // the k-th latest delayed value sits in slot (n - 1 - k) mod TW: one static rotation per n
+        auto fin = [&](auto rl_c) {
+          constexpr int RL = decltype(rl_c)::value;
 #pragma unroll
-        for (int k = 0; k < TW; ++k) {
-          q = __builtin_fma(ring[k], ring[k], q);
-          v[k] += s2x2 - q;
-        }
+          for (int k = 0; k < TW; ++k) {
+            const double rk = ring[(RL - k) & (TW - 1)];
+            q = __builtin_fma(rk, rk, q);
+            v[k] += s2x2 - q;
+          }
+        };
+        static_dispatch<TW>((n - 1) & (TW - 1), fin);
         const double mean = r1 / n;
         const double dm = mean - sh;
         const double mm2 = (s2 - 2.0 * dm * s1) + n * (dm * dm);
