@@ -241,7 +241,7 @@ hmc_status hmc_variogram(const double* x, int64_t n_chains, int64_t chain_stride
  *   row 2 + t    sum_j sum_s (x_j[s+t] - x_j[s])^2, t = 1..tmax (variogram, :161-179; 0 for t >= n)
  * over the 2*n_chains split chains j (same strided view as hmc_split_moments), S_d = x[base + d]
  * (the view's first sample: a common shift so that B needs no second pass).  tmax in
- * {8, 16, 32, 64}; longer lags: hmc_variogram.  Deterministic (fixed-order two-stage sums). */
+ * {8, 16, 32, 48, 64}; longer lags: hmc_variogram.  Deterministic (fixed-order two-stage sums). */
 int64_t hmc_convergence_work_size(int64_t n_chains, int32_t D, int32_t tmax);
 hmc_status hmc_convergence_sums(const double* x, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
                                 int64_t base, int32_t n, int32_t D, int32_t tmax, double* work, double* out,

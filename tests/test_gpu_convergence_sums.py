@@ -42,6 +42,9 @@ CASES = [
     (9, 300, 101, 1, 1, 1, 64),        # D = 100 view, odd row stride -> register-staged kernel
     (9, 300, 100, -1, 1, 1, 64),       # even strides, storage at an 8-B offset -> register-staged
     (11, 120, 100, 0, 3, 0, 32),       # even stride x thin: LDS kernel on a thinned view
+    (7, 101, 100, 0, 1, 1, 48),        # n = 50 (the bench window), 48 lags: 3-wave blocks
+    (4, 201, 130, 0, 1, 1, 48),        # n = 100 > 48
+    (6, 101, 101, 0, 1, 1, 48),        # odd D, 48 lags -> register-staged kernel (an idle wave)
 ]
 
 
@@ -69,3 +72,24 @@ def test_convergence_sums_vs_numpy(N, Niter, Dtot, d0, thin, wu, tmax):
     view = q[:, wu::thin, d0:]
     want = _expected(view, sp.n, tmax)
     np.testing.assert_allclose(got, want, rtol=1e-10, atol=1e-9 * np.abs(want).max())
+
+
+@pytest.mark.parametrize("D", [100, 7])
+def test_convergence_stats_n50_vs_oracle(D):
+    """Split chains of n = 50 (the bench window) take 48 lags in the one pass (conv_tmax); the
+    dimensions whose ESS criterion reaches its final check (lag 49: slow mixing) read it from
+    hmc_variogram.  R-hat and ESS equal the oracle's (utils.py:77-179 restated)."""
+    from hmc_amd import diagnostics as G
+    from oracle import hmc_oracle as O
+    rs = np.random.RandomState(5)
+    N, L = 24, 101
+    rho = np.linspace(0.0, 0.995, D)
+    x = np.empty((N, L, D))
+    x[:, 0] = rs.standard_normal((N, D)) - 2.0
+    for t in range(1, L):
+        x[:, t] = -2.0 + rho * (x[:, t - 1] + 2.0) + np.sqrt(1 - rho * rho) * rs.standard_normal((N, D))
+    R, neff = G.convergence_stats(x[:, 1:, :], thin_rate=1, warm_up_num=0)
+    assert G.LAST_INFO["tmax"] == 48 and G.LAST_INFO["fallback_dims"] > 0
+    R_ref, neff_ref = O.convergence_stats(x[:, 1:, :], thin_rate=1, warm_up_num=0)
+    np.testing.assert_allclose(R, R_ref, rtol=1e-10)
+    np.testing.assert_allclose(neff, neff_ref, rtol=1e-8)

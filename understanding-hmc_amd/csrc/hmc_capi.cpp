@@ -434,7 +434,7 @@ hmc_status hmc_variogram(const double* x, int64_t n_chains, int64_t chain_stride
                     "hmc_variogram");
 }
 
-static bool conv_tmax_ok(int32_t t) { return t == 8 || t == 16 || t == 32 || t == 64; }
+static bool conv_tmax_ok(int32_t t) { return t == 8 || t == 16 || t == 32 || t == 48 || t == 64; }
 
 int64_t hmc_convergence_work_size(int64_t n_chains, int32_t D, int32_t tmax) {
   if (n_chains < 1 || D < 1 || !conv_tmax_ok(tmax)) return 0;
@@ -445,7 +445,7 @@ hmc_status hmc_convergence_sums(const double* x, int64_t n_chains, int64_t chain
                                 int64_t base, int32_t n, int32_t D, int32_t tmax, double* work, double* out,
                                 void* stream) {
   if (!x || !work || !out || n_chains < 1 || n < 2 || D < 1) return fail(HMC_EINVAL, "bad arguments");
-  if (!conv_tmax_ok(tmax)) return fail(HMC_EINVAL, "tmax must be 8, 16, 32 or 64");
+  if (!conv_tmax_ok(tmax)) return fail(HMC_EINVAL, "tmax must be 8, 16, 32, 48 or 64");
   return hip_status(hmc::launch_conv_fused(x, n_chains, chain_stride, sample_stride, base, n, D, tmax, work, out,
                                            (hipStream_t)stream),
                     "hmc_convergence_sums");
@@ -463,7 +463,7 @@ hmc_status hmc_stream_accumulate(const double* window, int64_t n_chains, int64_t
   if (!window || !shift || !s1 || !s2 || !work || !vsum || n_chains < 1 || D < 1 || rows < 0 || carry < 0 ||
       n_half < 2 || pos0 < 0 || wrap < 1 || slot0 < 0 || slot0 >= wrap || carry + rows > wrap)
     return fail(HMC_EINVAL, "bad arguments");
-  if (tmax != 8 && tmax != 16 && tmax != 32 && tmax != 64) return fail(HMC_EINVAL, "tmax must be 8, 16, 32 or 64");
+  if (tmax != 8 && tmax != 16 && tmax != 32 && tmax != 64) return fail(HMC_EINVAL, "tmax must be 8, 16, 32, 48 or 64");
   if (carry < (pos0 < tmax ? pos0 : tmax)) return fail(HMC_EINVAL, "carry must be >= min(tmax, pos0)");
   if (rows == 0) return HMC_OK;
   return hip_status(hmc::launch_stream_accum(window, n_chains, chain_stride, sample_stride, D, wrap, slot0, carry, rows,

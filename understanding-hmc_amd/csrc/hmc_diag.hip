@@ -216,7 +216,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
   for (int k = 0; k < TW; ++k) v[k] = 0.0;
   double a_std = 0.0, a_m = 0.0, a_m2 = 0.0;
-  if (d < s.D && grp < groups) {
+  if (d < s.D && grp < groups && slot < SL) {   // (G = 3: the fourth wave idles)
     const double S = s.x[s.base + d];
     const int pos_suf = n - gofs - 1;   // T_t needs S2 through this position
     for (int64_t j = (int64_t)grp * SL + slot; j < m2; j += (int64_t)groups * SL) {
@@ -306,15 +306,36 @@ __device__ __forceinline__ void static_dispatch(int r, F& f) {
   static_dispatch_(r, f, std::make_integer_sequence<int, N>{});
 }
 
+// s_waitcnt vmcnt(c) for a wave-uniform c in [0, 8]
+__device__ __forceinline__ void wait_vmcnt(int c) {
+  switch (c) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+  }
+}
+
+// waves per block, and waves per SIMD (the launch bound: registers) of k_conv_lds<TW, G, 2>; the
+// LDS ring allows 4 / 3 / 2 / 1 / 3 blocks per CU for G = 3 / 4 / 2 / 1 (TW 16) / 1 (TW 8)
+constexpr int conv_waves(int G) { return G == 3 ? 3 : 4; }
+constexpr int conv_wpe(int TW, int G) { return G >= 3 ? 3 : G == 2 ? 2 : TW == 16 ? 1 : 3; }
+
 template <int TW, int G, int PD>
-__global__ __launch_bounds__(256, 3) void k_conv_lds(Src s, int groups, int ntiles, double* partial) {
-  constexpr int SL = 4 / G;                       // split chains per block at a time
+__global__ __launch_bounds__(64 * conv_waves(G), conv_wpe(TW, G)) void k_conv_lds(Src s, int groups, int ntiles,
+                                                                                  double* partial) {
+  constexpr int NW = conv_waves(G);               // waves per block
+  constexpr int SL = NW / G;                      // split chains per block at a time
   constexpr int T = TW * G;
   constexpr int RB = (G + PD) * TW;               // ring rows per slot (multiple of TW)
-  constexpr int NI = TW / 2 / G;                  // DMA instructions per wave and chunk (2 rows each)
-  static_assert(NI >= 1 && NI * 2 * G == TW, "TW must be a multiple of 2G");
-  __shared__ double ring_x[SL * RB * kDimTile];
-  __shared__ double red[4][kDimTile];
+  constexpr int NP = TW / 2;                      // DMA instructions per chunk (2 rows each)
+  static_assert(SL * G == NW && TW % 2 == 0 && (TW & (TW - 1)) == 0, "layout");
+  __shared__ double ring_x[SL * RB * kDimTile];   // (the final reduction reuses it)
   const int lane = threadIdx.x & (kDimTile - 1);
   const int dl = lane;
   const int w = threadIdx.x / kDimTile;
@@ -332,20 +353,23 @@ __global__ __launch_bounds__(256, 3) void k_conv_lds(Src s, int groups, int ntil
   const int K = grp < groups ? (int)((m2 - j0 + stride - 1) / stride) : 0;   // split chains per slot (max)
   const int F = K * nch;                          // (split chain, chunk) items, the same for all slots
   double* const my = ring_x + slot * RB * kDimTile;
-  // DMA of item f into ring rows (f TW) % RB ...: wave g moves rows 2(g + G e), +1 of the chunk
+  // DMA of item f into ring rows (f TW) % RB ...: wave g moves row pairs g, g + G, ... of the chunk
+  const int ni = (NP - g + G - 1) / G;            // this wave's DMA instructions per chunk
   const int drow = lane >> 5, dcol = (lane & 31) * 2;   // this lane's row (of 2) and dim pair
   auto issue = [&](int f) {
     const int64_t j = j0 + slot + (int64_t)(f / nch) * stride;
     const int cc = f % nch;
     const int r0 = (f * TW) % RB;
 #pragma unroll
-    for (int e = 0; e < NI; ++e) {
+    for (int e = 0; e < (NP + G - 1) / G; ++e) {
       const int rr = 2 * (g + G * e);             // row pair inside the chunk
-      const int row = cc * TW + rr + drow;
-      const bool ok = j < m2 && row < n && tile * kDimTile + dcol < s.D;   // D even: whole pairs
-      const double* src = ok ? split_ptr(s, j, row) + tile * kDimTile + dcol : s.x + s.base;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(my + (r0 + rr) * kDimTile),
-                                       16, 0, 0);
+      if (rr < TW) {
+        const int row = cc * TW + rr + drow;
+        const bool ok = j < m2 && row < n && tile * kDimTile + dcol < s.D;   // D even: whole pairs
+        const double* src = ok ? split_ptr(s, j, row) + tile * kDimTile + dcol : s.x + s.base;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(my + (r0 + rr) * kDimTile),
+                                         16, 0, 0);
+      }
     }
   };
   double v[TW];
@@ -353,18 +377,16 @@ __global__ __launch_bounds__(256, 3) void k_conv_lds(Src s, int groups, int ntil
   for (int k = 0; k < TW; ++k) v[k] = 0.0;
   double a_std = 0.0, a_m = 0.0, a_m2 = 0.0;
   const double S = d < s.D ? s.x[s.base + d] : 0.0;
+  // ring slot i holds -2 (x_delayed - shift) of chunk row i (the chunks are TW-aligned), so at row
+  // i lag gofs + 1 + k reads slot (i - 1 - k) mod TW: static registers, no ring shifts, and the
+  // lag product is one FMA (-2 y x_d: scaling by -2 is exact)
   double ring[TW];
-  double sh = 0.0, s1 = 0.0, s2 = 0.0, r1 = 0.0, sufb = 0.0;
+  double sh = 0.0, sh2 = 0.0, s1 = 0.0, s2 = 0.0, r1 = 0.0, sufb = 0.0;
   const int pos_suf = n - gofs - 1;
   for (int f = 0; f < PD && f < F; ++f) issue(f);
   for (int f = 0; f < F; ++f) {
     // item f's rows have landed (PD - 1 newer items may still fly), and every wave is past item f-1
-    if (f + PD - 1 < F) {
-      if constexpr (PD == 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NI) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    wait_vmcnt(f + PD - 1 < F ? (PD - 1) * ni : 0);
     __builtin_amdgcn_s_barrier();
     if (f + PD < F) issue(f + PD);
     const int64_t j = j0 + slot + (int64_t)(f / nch) * stride;
@@ -374,42 +396,51 @@ __global__ __launch_bounds__(256, 3) void k_conv_lds(Src s, int groups, int ntil
     if (j < m2 && d < s.D) {
       if (cc == 0) {                              // a split chain starts
         sh = my[rc * kDimTile + dl];
+        sh2 = 2.0 * sh;
 #pragma unroll
         for (int k = 0; k < TW; ++k) ring[k] = 0.0;
         s1 = s2 = r1 = sufb = 0.0;
       }
-      // ring slot i holds the delayed value of chunk row i (the chunks are TW-aligned), so at row i
-      // lag gofs + 1 + k reads slot (i - 1 - k) mod TW: static registers, no ring shifts
       const int rem = n - cc * TW;                // rows of this chunk
       const bool hwin = cc * TW == gofs;          // this chunk's running S2 gives H_t of our lags
       const bool dly = cc * TW >= gofs;           // the delayed rows exist (gofs is a multiple of TW)
       const int isuf = pos_suf - cc * TW;         // suffix mark (T_t terms), if inside this chunk
-      auto rows = [&](auto plain_c) {
+      auto rows = [&](auto plain_c, auto mom_c) {
         constexpr bool PLAIN = decltype(plain_c)::value;   // whole chunk, no H_t / suffix event
+        constexpr bool MOM = decltype(mom_c)::value;       // lag group 0 also sums the moments
 #pragma unroll
         for (int i = 0; i < TW; ++i) {
           if (PLAIN || i < rem) {
             const double x = my[(rc + i) * kDimTile + dl];
             const double xd = dly ? my[(rd + i) * kDimTile + dl] : sh;
-            r1 += x;
             const double y = x - sh;
-            s1 += y;
+            if constexpr (MOM) {
+              r1 += x;
+              s1 += y;
+            }
             s2 = __builtin_fma(y, y, s2);
-            const double ym2 = -2.0 * y;
 #pragma unroll
-            for (int k = 0; k < TW; ++k) v[k] = __builtin_fma(ym2, ring[(i - 1 - k) & (TW - 1)], v[k]);
+            for (int k = 0; k < TW; ++k) v[k] = __builtin_fma(y, ring[(i - 1 - k) & (TW - 1)], v[k]);
             if (!PLAIN) {
               if (hwin) v[i] -= s2;
               if (i == isuf) sufb = s2;
             }
-            ring[i] = xd - sh;
+            ring[i] = __builtin_fma(-2.0, xd, sh2);   // -2 (xd - sh), one rounding: exact scaling
           }
         }
       };
-      if (rem >= TW && !hwin && (isuf < 0 || isuf >= TW)) rows(std::true_type{});
-      else rows(std::false_type{});
+      const bool plain = rem >= TW && !hwin && (isuf < 0 || isuf >= TW);
+      if (g == 0) {
+        if (plain) rows(std::true_type{}, std::true_type{});
+        else rows(std::false_type{}, std::true_type{});
+      } else {
+        if (plain) rows(std::true_type{}, std::false_type{});
+        else rows(std::false_type{}, std::false_type{});
+      }
       if (cc == nch - 1) {                        // the split chain is complete
-        double q = pos_suf >= 0 ? s2 - sufb : s2;
+        // q4 = 4 (S2 - S2 through n-1-gofs) + sum of the ring's (-2 y)^2: 4x the T_t suffix sums,
+        // exactly (power-of-2 scalings commute with rounding)
+        double q4 = 4.0 * (pos_suf >= 0 ? s2 - sufb : s2);
         const double s2x2 = 2.0 * s2;
         // the k-th latest delayed value sits in slot (n - 1 - k) mod TW: one static rotation per n
         auto fin = [&](auto rl_c) {
@@ -417,27 +448,35 @@ __global__ __launch_bounds__(256, 3) void k_conv_lds(Src s, int groups, int ntil
 #pragma unroll
           for (int k = 0; k < TW; ++k) {
             const double rk = ring[(RL - k) & (TW - 1)];
-            q = __builtin_fma(rk, rk, q);
-            v[k] += s2x2 - q;
+            q4 = __builtin_fma(rk, rk, q4);
+            v[k] += __builtin_fma(-0.25, q4, s2x2);
           }
         };
         static_dispatch<TW>((n - 1) & (TW - 1), fin);
-        const double mean = r1 / n;
-        const double dm = mean - sh;
-        const double mm2 = (s2 - 2.0 * dm * s1) + n * (dm * dm);
-        a_std += sqrt(mm2 > 0.0 ? mm2 / (n - 1) : 0.0);
-        const double e = mean - S;
-        a_m += e;
-        a_m2 = __builtin_fma(e, e, a_m2);
+        if (g == 0) {
+          const double mean = r1 / n;
+          const double dm = mean - sh;
+          const double mm2 = (s2 - 2.0 * dm * s1) + n * (dm * dm);
+          a_std += sqrt(mm2 > 0.0 ? mm2 / (n - 1) : 0.0);
+          const double e = mean - S;
+          a_m += e;
+          a_m2 = __builtin_fma(e, e, a_m2);
+        }
       }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();                                // every wave is done with the ring
+  double* const red = ring_x;                     // [NW][kDimTile]
   auto put = [&](int row, double x) {
-    red[w][dl] = x;
+    red[w * kDimTile + dl] = x;
     __syncthreads();
-    if (w == 0 && d < s.D && grp < groups)
-      partial[((int64_t)grp * (T + 3) + row) * s.D + d] = ((red[0][dl] + red[1][dl]) + red[2][dl]) + red[3][dl];
+    if (w == 0 && d < s.D && grp < groups) {
+      double acc = red[dl];
+#pragma unroll
+      for (int ww = 1; ww < NW; ++ww) acc += red[ww * kDimTile + dl];
+      partial[((int64_t)grp * (T + 3) + row) * s.D + d] = acc;
+    }
     __syncthreads();
   };
   put(0, g == 0 ? a_std : 0.0);
@@ -624,7 +663,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T <= 16 ? 3
 int64_t rows_chunks(int64_t rows) { return (rows + kRowChunk - 1) / kRowChunk; }
 
 // Blocks resident per CU for the lag kernel of T lags (LDS ring and VGPRs; see the launch switch).
-constexpr int conv_blocks_per_cu(int T) { return T == 16 ? 1 : T == 32 ? 2 : 3; }
+constexpr int conv_blocks_per_cu(int T) { return T == 16 ? 1 : T == 32 ? 2 : T == 48 ? 4 : 3; }
 
 // Block groups of the lag pass: one resident wave of blocks over all dim tiles (no tail wave).
 int64_t conv_groups(int64_t n_chains, int D, int T) {
@@ -687,6 +726,7 @@ hipError_t launch_conv_fused(const double* x, int64_t n_chains, int64_t cs, int6
       case 8: k_conv_lags<8, 1><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
       case 16: k_conv_lags<16, 1><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
       case 32: k_conv_lags<16, 2><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
+      case 48: k_conv_lags<16, 3><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
       case 64: k_conv_lags<16, 4><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
       default: return hipErrorInvalidValue;
     }
@@ -694,6 +734,7 @@ hipError_t launch_conv_fused(const double* x, int64_t n_chains, int64_t cs, int6
     case 8: k_conv_lds<8, 1, 2><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
     case 16: k_conv_lds<16, 1, 2><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
     case 32: k_conv_lds<16, 2, 2><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
+    case 48: k_conv_lds<16, 3, 2><<<grid, 192, 0, st>>>(s, (int)groups, ntiles, work); break;
     case 64: k_conv_lds<16, 4, 2><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
     default: return hipErrorInvalidValue;
   }

@@ -109,6 +109,19 @@ def convergence_sums(sp, tmax):
     return out
 
 
+_TMAX = (8, 16, 32, 48, 64)
+
+
+def conv_tmax(n):
+    """Lags of the one-pass sums for split chains of n samples: every lag t < n when they fit,
+    except that a lag group (16 lags, one more wave per split chain) is not spent on the last one or
+    two lags: the ESS criterion reads lag n - 1 only in its final check (t = n - 3), and the
+    dimensions that get that far read the missing lags from hmc_variogram (exact either way)."""
+    fit = next((t for t in _TMAX if t >= n - 1), _TMAX[-1])
+    lower = [t for t in _TMAX if t < fit]
+    return lower[-1] if lower and lower[-1] >= n - 3 and lower[-1] >= 32 else fit
+
+
 def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
     """utils.py:77-159 on the GPU.  q_chain: (Nchain, Niter, D) NumPy array or CUDA tensor
     (views such as q_chain_device[:, 1:, :] are read in place).  Returns (R, n_eff) NumPy.
@@ -121,7 +134,7 @@ def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
     sp = _Split(q_chain, thin_rate, warm_up_num)
     n, D = sp.n, sp.D
     dev = sp.t.device
-    tmax = next((t for t in (8, 16, 32, 64) if t >= n - 1), 64)   # all lags t < n when they fit
+    tmax = conv_tmax(n)
     sums = convergence_sums(sp, tmax)
     S = sp.t.reshape(-1)[sp.base:sp.base + D].to(torch.float64)          # the kernels' shift S_d
     m_loc = 2 * sp.Nchain
