@@ -24,3 +24,21 @@ for r in range(reps):
     torch.cuda.synchronize()
     print(f"rep {r}: {time.perf_counter() - t0:.4f} s  info={G.LAST_INFO}  rhat_med={np.median(Rh):.5f} "
           f"neff_med={np.median(ne):.4e}", flush=True)
+
+# the one-pass kernel alone, per lag width (HIP events), with board power / clock while it runs
+if os.environ.get("DIAG_KERNEL"):
+    from bench import Telemetry  # noqa: E402
+    sp = G._Split(x, 1, 0)
+    for tm in [int(t) for t in os.environ["DIAG_KERNEL"].split(",")]:
+        G.convergence_sums(sp, tm)
+        torch.cuda.synchronize()
+        tel = Telemetry(0, 0.005).start()
+        ts = []
+        for r in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            G.convergence_sums(sp, tm)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        print(f"tmax {tm}: ms {[round(t, 2) for t in ts]}  telemetry {tel.stop()}", flush=True)
