@@ -234,11 +234,13 @@ hmc_status hmc_variogram(const double* x, int64_t n_chains, int64_t chain_stride
                          void* stream);
 
 /* Everything convergence_stats needs from the samples in ONE pass (utils.py:88-126, :161-179):
- * out[(3 + tmax)][D] =
+ * out[(4 + tmax)][D] =
  *   row 0        sum_j std_j (ddof=1)                       (W, utils.py:109-112)
  *   row 1        sum_j (mean_j - S_d)                       (mean_all, :116-119)
  *   row 2        sum_j (mean_j - S_d)^2                     (B, :120, after re-centring)
  *   row 2 + t    sum_j sum_s (x_j[s+t] - x_j[s])^2, t = 1..tmax (variogram, :161-179; 0 for t >= n)
+ *   row 3 + tmax sum_j (x_j[n-1] - x_j[0])^2: the variogram of lag n - 1, the last lag the ESS loop
+ *                reads (:139-150), whatever tmax (0 for n < 2)
  * over the 2*n_chains split chains j (same strided view as hmc_split_moments), S_d = x[base + d]
  * (the view's first sample: a common shift so that B needs no second pass).  tmax in
  * {8, 16, 32, 48, 64}; longer lags: hmc_variogram.  Deterministic (fixed-order two-stage sums). */

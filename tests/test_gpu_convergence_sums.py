@@ -5,7 +5,7 @@ one (odd D, odd strides, a misaligned view), n below / at / above the chunk and 
 or few split chains per block group, and every lag width tmax in {8, 16, 32, 64}.
 
 The sums are the ones include/hmc.h documents: rows [sum_j std_j, sum_j (mean_j - S),
-sum_j (mean_j - S)^2, V_1 .. V_tmax] with S = the view's first sample and
+sum_j (mean_j - S)^2, V_1 .. V_tmax, V_{n-1}] with S = the view's first sample and
 V_t = sum_j sum_{s < n-t} (x_j[s+t] - x_j[s])^2 (0 for t >= n)."""
 import numpy as np
 import pytest
@@ -21,12 +21,14 @@ def _expected(view, n, tmax):
     S = view[0, 0]
     mean = xs.mean(axis=1)
     std = xs.std(axis=1, ddof=1)
-    out = np.zeros((3 + tmax, D))
+    out = np.zeros((4 + tmax, D))
     out[0] = std.sum(axis=0)
     out[1] = (mean - S).sum(axis=0)
     out[2] = ((mean - S) ** 2).sum(axis=0)
     for t in range(1, min(tmax, n - 1) + 1):
         out[2 + t] = ((xs[:, t:] - xs[:, :-t]) ** 2).sum(axis=(0, 1))
+    if n >= 2:
+        out[3 + tmax] = ((xs[:, n - 1] - xs[:, 0]) ** 2).sum(axis=0)      # lag n - 1
     return out
 
 
@@ -76,9 +78,9 @@ def test_convergence_sums_vs_numpy(N, Niter, Dtot, d0, thin, wu, tmax):
 
 @pytest.mark.parametrize("D", [100, 7])
 def test_convergence_stats_n50_vs_oracle(D):
-    """Split chains of n = 50 (the bench window) take 48 lags in the one pass (conv_tmax); the
-    dimensions whose ESS criterion reaches its final check (lag 49: slow mixing) read it from
-    hmc_variogram.  R-hat and ESS equal the oracle's (utils.py:77-179 restated)."""
+    """Split chains of n = 50 (the bench window): the one pass takes lags 1..48 (conv_tmax) and
+    lag 49 (its extra row), so the dimensions whose ESS criterion reaches its final check (slow
+    mixing) need no further pass.  R-hat and ESS equal the oracle's (utils.py:77-179 restated)."""
     from hmc_amd import diagnostics as G
     from oracle import hmc_oracle as O
     rs = np.random.RandomState(5)
@@ -89,7 +91,7 @@ def test_convergence_stats_n50_vs_oracle(D):
     for t in range(1, L):
         x[:, t] = -2.0 + rho * (x[:, t - 1] + 2.0) + np.sqrt(1 - rho * rho) * rs.standard_normal((N, D))
     R, neff = G.convergence_stats(x[:, 1:, :], thin_rate=1, warm_up_num=0)
-    assert G.LAST_INFO["tmax"] == 48 and G.LAST_INFO["fallback_dims"] > 0
+    assert G.LAST_INFO["tmax"] == 48 and G.LAST_INFO["lags"] == 49 and G.LAST_INFO["fallback_dims"] == 0
     R_ref, neff_ref = O.convergence_stats(x[:, 1:, :], thin_rate=1, warm_up_num=0)
     np.testing.assert_allclose(R, R_ref, rtol=1e-10)
     np.testing.assert_allclose(neff, neff_ref, rtol=1e-8)

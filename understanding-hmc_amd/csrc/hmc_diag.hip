@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   double v[TW];
 #pragma unroll
   for (int k = 0; k < TW; ++k) v[k] = 0.0;
-  double a_std = 0.0, a_m = 0.0, a_m2 = 0.0;
+  double a_std = 0.0, a_m = 0.0, a_m2 = 0.0, a_last = 0.0;
   if (d < s.D && grp < groups && slot < SL) {   // (G = 3: the fourth wave idles)
     const double S = s.x[s.base + d];
     const int pos_suf = n - gofs - 1;   // T_t needs S2 through this position
@@ -269,13 +269,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       const double e = mean - S;
       a_m += e;
       a_m2 = __builtin_fma(e, e, a_m2);
+      const double yl = bp[(int64_t)(n - 1) * ss] - sh;   // lag n - 1: (x[n-1] - x[0])^2
+      a_last = __builtin_fma(yl, yl, a_last);
     }
   }
   auto put = [&](int row, double x) {
     red[w][dl] = x;
     __syncthreads();
     if (w == 0 && d < s.D && grp < groups)
-      partial[((int64_t)grp * (T + 3) + row) * s.D + d] = ((red[0][dl] + red[1][dl]) + red[2][dl]) + red[3][dl];
+      partial[((int64_t)grp * (T + 4) + row) * s.D + d] = ((red[0][dl] + red[1][dl]) + red[2][dl]) + red[3][dl];
     __syncthreads();
   };
   put(0, g == 0 ? a_std : 0.0);
@@ -286,6 +288,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
     for (int k = 0; k < TW; ++k) put(3 + gg * TW + k, g == gg && gg * TW + k + 1 < s.n ? v[k] : 0.0);   // lags t >= n: 0
   }
+  put(3 + T, g == 0 && s.n >= 2 ? a_last : 0.0);  // lag n - 1 (the ESS loop's last), whatever T
 }
 
 // The same sums with the series staged through LDS: each block runs SL = 4/G split chains at a time
@@ -375,7 +378,7 @@ __global__ __launch_bounds__(64 * conv_waves(G), conv_wpe(TW, G)) void k_conv_ld
   double v[TW];
 #pragma unroll
   for (int k = 0; k < TW; ++k) v[k] = 0.0;
-  double a_std = 0.0, a_m = 0.0, a_m2 = 0.0;
+  double a_std = 0.0, a_m = 0.0, a_m2 = 0.0, a_last = 0.0;
   const double S = d < s.D ? s.x[s.base + d] : 0.0;
   // ring slot i holds -2 (x_delayed - shift) of chunk row i (the chunks are TW-aligned), so at row
   // i lag gofs + 1 + k reads slot (i - 1 - k) mod TW: static registers, no ring shifts, and the
@@ -461,6 +464,8 @@ __global__ __launch_bounds__(64 * conv_waves(G), conv_wpe(TW, G)) void k_conv_ld
           const double e = mean - S;
           a_m += e;
           a_m2 = __builtin_fma(e, e, a_m2);
+          const double yl = my[(rc + rem - 1) * kDimTile + dl] - sh;   // lag n - 1: (x[n-1] - x[0])^2
+          a_last = __builtin_fma(yl, yl, a_last);
         }
       }
     }
@@ -475,7 +480,7 @@ __global__ __launch_bounds__(64 * conv_waves(G), conv_wpe(TW, G)) void k_conv_ld
       double acc = red[dl];
 #pragma unroll
       for (int ww = 1; ww < NW; ++ww) acc += red[ww * kDimTile + dl];
-      partial[((int64_t)grp * (T + 3) + row) * s.D + d] = acc;
+      partial[((int64_t)grp * (T + 4) + row) * s.D + d] = acc;
     }
     __syncthreads();
   };
@@ -487,6 +492,7 @@ __global__ __launch_bounds__(64 * conv_waves(G), conv_wpe(TW, G)) void k_conv_ld
 #pragma unroll
     for (int k = 0; k < TW; ++k) put(3 + gg * TW + k, g == gg && gg * TW + k + 1 < s.n ? v[k] : 0.0);   // lags t >= n: 0
   }
+  put(3 + T, g == 0 && s.n >= 2 ? a_last : 0.0);  // lag n - 1 (the ESS loop's last), whatever T
 }
 
 // ---- streaming (windowed) split-chain statistics: q_chain never has to be stored whole.
@@ -663,7 +669,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T <= 16 ? 3
 int64_t rows_chunks(int64_t rows) { return (rows + kRowChunk - 1) / kRowChunk; }
 
 // Blocks resident per CU for the lag kernel of T lags (LDS ring and VGPRs; see the launch switch).
+#ifdef HMC_CONV48_BPC3   // A/B: 48-lag grid sized for 3 blocks per CU
+constexpr int conv_blocks_per_cu(int T) { return T == 16 ? 1 : T == 32 ? 2 : 3; }
+#else
 constexpr int conv_blocks_per_cu(int T) { return T == 16 ? 1 : T == 32 ? 2 : T == 48 ? 4 : 3; }
+#endif
 
 // Block groups of the lag pass: one resident wave of blocks over all dim tiles (no tail wave).
 int64_t conv_groups(int64_t n_chains, int D, int T) {
@@ -710,7 +720,7 @@ hipError_t launch_rowsum(const double* x, int64_t n_outer, int64_t os, int64_t n
   return hipGetLastError();
 }
 
-int64_t diag_conv_work(int64_t n_chains, int D, int T) { return conv_groups(n_chains, D, T) * (int64_t)(T + 3) * D; }
+int64_t diag_conv_work(int64_t n_chains, int D, int T) { return conv_groups(n_chains, D, T) * (int64_t)(T + 4) * D; }
 
 hipError_t launch_conv_fused(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int64_t base, int n, int D,
                              int T, double* work, double* out, hipStream_t st) {
@@ -739,7 +749,7 @@ hipError_t launch_conv_fused(const double* x, int64_t n_chains, int64_t cs, int6
     default: return hipErrorInvalidValue;
   }
   if (hipError_t e = hipGetLastError()) return e;
-  const int64_t ncols = (int64_t)(T + 3) * D;
+  const int64_t ncols = (int64_t)(T + 4) * D;
   k_colsum_final<<<(unsigned)((ncols + 255) / 256), 256, 0, st>>>(work, groups, ncols, out);
   return hipGetLastError();
 }

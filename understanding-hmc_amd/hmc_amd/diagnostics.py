@@ -97,13 +97,13 @@ def variogram_sums(sp, t0, t1):
 
 
 def convergence_sums(sp, tmax):
-    """One pass over the samples (C-ABI hmc_convergence_sums): (3 + tmax, D) device tensor of
-    sum_j std_j, sum_j (mean_j - S), sum_j (mean_j - S)^2 and the variogram sums of lags 1..tmax,
-    S = the view's first sample (see include/hmc.h)."""
+    """One pass over the samples (C-ABI hmc_convergence_sums): (4 + tmax, D) device tensor of
+    sum_j std_j, sum_j (mean_j - S), sum_j (mean_j - S)^2, the variogram sums of lags 1..tmax and
+    that of lag n - 1, S = the view's first sample (see include/hmc.h)."""
     L = H.lib()
     work = torch.empty(max(1, L.hmc_convergence_work_size(sp.Nchain, sp.D, tmax)), dtype=torch.float64,
                        device=sp.t.device)
-    out = torch.empty((3 + tmax, sp.D), dtype=torch.float64, device=sp.t.device)
+    out = torch.empty((4 + tmax, sp.D), dtype=torch.float64, device=sp.t.device)
     H.check(L.hmc_convergence_sums(sp.ptr, sp.Nchain, sp.cs, sp.ss, sp.base, sp.n, sp.D, tmax, H.ptr(work),
                                    H.ptr(out), _stream(sp.t)), "hmc_convergence_sums")
     return out
@@ -113,13 +113,11 @@ _TMAX = (8, 16, 32, 48, 64)
 
 
 def conv_tmax(n):
-    """Lags of the one-pass sums for split chains of n samples: every lag t < n when they fit,
-    except that a lag group (16 lags, one more wave per split chain) is not spent on the last one or
-    two lags: the ESS criterion reads lag n - 1 only in its final check (t = n - 3), and the
-    dimensions that get that far read the missing lags from hmc_variogram (exact either way)."""
-    fit = next((t for t in _TMAX if t >= n - 1), _TMAX[-1])
-    lower = [t for t in _TMAX if t < fit]
-    return lower[-1] if lower and lower[-1] >= n - 3 and lower[-1] >= 32 else fit
+    """Lag groups of the one-pass sums for split chains of n samples: lags 1..tmax, tmax the
+    smallest width >= n - 2, since the pass always adds lag n - 1 (one square per split chain), so
+    every lag t < n is there when n <= 66 (n = 50, the bench window: 48 lags, three waves per split
+    chain instead of four)."""
+    return next((t for t in _TMAX if t >= n - 2), _TMAX[-1])
 
 
 def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
@@ -127,10 +125,11 @@ def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
     (views such as q_chain_device[:, 1:, :] are read in place).  Returns (R, n_eff) NumPy.
 
     One pass over the samples gives every per-dimension sum R-hat needs and the variogram of every
-    lag t < n up to 64 (hmc_convergence_sums); the ESS termination (utils.py:130-157) runs vectorised
-    over the dimensions on the host, and only dimensions whose criterion has not fired by then
-    (n > 65 and slow mixing) read further lag blocks (hmc_variogram).  Ranks all-reduce the per-dimension sums: two rounds, B needs the
-    global mean."""
+    lag t < n up to 64, and of lag n - 1 (hmc_convergence_sums); the ESS termination
+    (utils.py:130-157) runs vectorised over the dimensions on the host, and only dimensions whose
+    criterion has not fired by then (n > 66 and slow mixing) read further lag blocks
+    (hmc_variogram).  Ranks all-reduce the per-dimension sums: two rounds, B needs the global
+    mean."""
     sp = _Split(q_chain, thin_rate, warm_up_num)
     n, D = sp.n, sp.D
     dev = sp.t.device
@@ -152,12 +151,14 @@ def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
     B = bsum * n / float(m - 1)                                         # :120
     var = W * (n - 1) / float(n) + B / float(n)                         # :123
     R = torch.sqrt(var / W)                                             # :126
-    v = r1[2:2 + tmax].cpu().numpy()
+    v = r1[2:3 + tmax].cpu().numpy()                                    # lags 1..tmax, then lag n - 1
     var_h = var.cpu().numpy()
     # ---- ESS (utils.py:128-157), vectorised over dims; more lags only where still undecided
     lmax = max(n - 1, 2)                                                # lags t < n exist
     T = min(tmax, lmax)
-    Vt = v[:T] / (m * (n - np.arange(1, T + 1)))[:, None]               # utils.py:177
+    v = np.vstack([v[:T], v[tmax:tmax + 1]]) if T == n - 2 else v[:T]  # + lag n - 1: complete
+    T = v.shape[0]
+    Vt = v / (m * (n - np.arange(1, T + 1)))[:, None]                   # utils.py:177
     n_eff, need = ess_vectorised(Vt, var_h, n, m, complete=T >= lmax)
     LAST_INFO.update(tmax=tmax, lags=T, fallback_dims=int(need.sum()), fallback_passes=0)
     if need.any():
