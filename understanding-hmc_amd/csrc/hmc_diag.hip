@@ -309,19 +309,12 @@ __device__ __forceinline__ void static_dispatch(int r, F& f) {
   static_dispatch_(r, f, std::make_integer_sequence<int, N>{});
 }
 
-// s_waitcnt vmcnt(c) for a wave-uniform c in [0, 8]
-__device__ __forceinline__ void wait_vmcnt(int c) {
-  switch (c) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-  }
+// this lane's id in its wave, recomputed where it is used (volatile: never kept live across a
+// loop, which costs two VALU instead of a register or a scratch reload)
+__device__ __forceinline__ int lane_id() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
 }
 
 // waves per block, and waves per SIMD (the launch bound: registers) of k_conv_lds<TW, G, 2>; the
@@ -357,22 +350,27 @@ __global__ __launch_bounds__(64 * conv_waves(G), conv_wpe(TW, G)) void k_conv_ld
   const int F = K * nch;                          // (split chain, chunk) items, the same for all slots
   double* const my = ring_x + slot * RB * kDimTile;
   // DMA of item f into ring rows (f TW) % RB ...: wave g moves row pairs g, g + G, ... of the chunk
-  const int ni = (NP - g + G - 1) / G;            // this wave's DMA instructions per chunk
-  const int drow = lane >> 5, dcol = (lane & 31) * 2;   // this lane's row (of 2) and dim pair
+  constexpr int NI = (NP + G - 1) / G;            // DMA instructions per wave and chunk (G = 3: the
+                                                  // last wave repeats pair NP - 1: same bytes, same place)
+  const int dcol = (lane & 31) * 2;               // this lane's dim pair (and row lane >> 5 of 2)
+  // per-lane part of a DMA address: this lane's dim pair (pair 0 for the dims past D: loaded,
+  // never read), and rows clamped into the split chain (rows past n are loaded, never read)
+  const int dofs = tile * kDimTile + dcol < s.D ? tile * kDimTile + dcol : 0;
   auto issue = [&](int f) {
     const int64_t j = j0 + slot + (int64_t)(f / nch) * stride;
     const int cc = f % nch;
+    const double* rb = split_ptr(s, j < m2 ? j : m2 - 1, 0);   // wave-uniform
+    rb = reinterpret_cast<const double*>(
+        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)rb >> 32)) << 32) |
+        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)rb));
     const int r0 = (f * TW) % RB;
 #pragma unroll
-    for (int e = 0; e < (NP + G - 1) / G; ++e) {
-      const int rr = 2 * (g + G * e);             // row pair inside the chunk
-      if (rr < TW) {
-        const int row = cc * TW + rr + drow;
-        const bool ok = j < m2 && row < n && tile * kDimTile + dcol < s.D;   // D even: whole pairs
-        const double* src = ok ? split_ptr(s, j, row) + tile * kDimTile + dcol : s.x + s.base;
-        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(my + (r0 + rr) * kDimTile),
-                                         16, 0, 0);
-      }
+    for (int e = 0; e < NI; ++e) {
+      const int rr = 2 * min(g + G * e, NP - 1);  // row pair inside the chunk
+      const int row = min(cc * TW + rr + (lane_id() >> 5), n - 1);
+      const double* src = rb + (int64_t)row * s.sample_stride + dofs;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(my + (r0 + rr) * kDimTile),
+                                       16, 0, 0);
     }
   };
   double v[TW];
@@ -380,6 +378,8 @@ __global__ __launch_bounds__(64 * conv_waves(G), conv_wpe(TW, G)) void k_conv_ld
   for (int k = 0; k < TW; ++k) v[k] = 0.0;
   double a_std = 0.0, a_m = 0.0, a_m2 = 0.0, a_last = 0.0;
   const double S = d < s.D ? s.x[s.base + d] : 0.0;
+  asm volatile("" ::"v"(S));                      // landed before the ring's loads are in flight: a
+                                                  // later first use would wait for vmcnt(0)
   // ring slot i holds -2 (x_delayed - shift) of chunk row i (the chunks are TW-aligned), so at row
   // i lag gofs + 1 + k reads slot (i - 1 - k) mod TW: static registers, no ring shifts, and the
   // lag product is one FMA (-2 y x_d: scaling by -2 is exact)
@@ -389,7 +389,8 @@ __global__ __launch_bounds__(64 * conv_waves(G), conv_wpe(TW, G)) void k_conv_ld
   for (int f = 0; f < PD && f < F; ++f) issue(f);
   for (int f = 0; f < F; ++f) {
     // item f's rows have landed (PD - 1 newer items may still fly), and every wave is past item f-1
-    wait_vmcnt(f + PD - 1 < F ? (PD - 1) * ni : 0);
+    if (f + PD - 1 < F) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((PD - 1) * NI) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (f + PD < F) issue(f + PD);
     const int64_t j = j0 + slot + (int64_t)(f / nch) * stride;
@@ -398,7 +399,7 @@ __global__ __launch_bounds__(64 * conv_waves(G), conv_wpe(TW, G)) void k_conv_ld
     const int rd = (rc - gofs + RB) % RB;         // ... of the delayed stream's
     if (j < m2 && d < s.D) {
       if (cc == 0) {                              // a split chain starts
-        sh = my[rc * kDimTile + dl];
+        sh = my[rc * kDimTile + lane_id()];
         sh2 = 2.0 * sh;
 #pragma unroll
         for (int k = 0; k < TW; ++k) ring[k] = 0.0;
@@ -411,11 +412,21 @@ __global__ __launch_bounds__(64 * conv_waves(G), conv_wpe(TW, G)) void k_conv_ld
       auto rows = [&](auto plain_c, auto mom_c) {
         constexpr bool PLAIN = decltype(plain_c)::value;   // whole chunk, no H_t / suffix event
         constexpr bool MOM = decltype(mom_c)::value;       // lag group 0 also sums the moments
+        // rows one ahead: row i + 1's two LDS reads are issued before row i's FMAs, and no later
+        // read moves above them (compiler fence), so at most two rows' values are live: a spill
+        // reload here would wait for vmcnt(0), i.e. for the ring's in-flight loads
+        const int ll = lane_id();                 // (recomputed: not worth a register)
+        double xn = my[rc * kDimTile + ll];
+        double xdn = dly ? my[rd * kDimTile + ll] : sh;
 #pragma unroll
         for (int i = 0; i < TW; ++i) {
+          const double x = xn, xd = xdn;
+          if (i + 1 < TW && (PLAIN || i + 1 < rem)) {
+            xn = my[(rc + i + 1) * kDimTile + ll];
+            xdn = dly ? my[(rd + i + 1) * kDimTile + ll] : sh;
+          }
+          asm volatile("" ::: "memory");
           if (PLAIN || i < rem) {
-            const double x = my[(rc + i) * kDimTile + dl];
-            const double xd = dly ? my[(rd + i) * kDimTile + dl] : sh;
             const double y = x - sh;
             if constexpr (MOM) {
               r1 += x;
@@ -457,14 +468,17 @@ __global__ __launch_bounds__(64 * conv_waves(G), conv_wpe(TW, G)) void k_conv_ld
         };
         static_dispatch<TW>((n - 1) & (TW - 1), fin);
         if (g == 0) {
-          const double mean = r1 / n;
+          int nn = n;
+          asm volatile("" : "+s"(nn));            // n's doubles: converted here, not kept in registers
+          const double dn = nn;
+          const double mean = r1 / dn;
           const double dm = mean - sh;
-          const double mm2 = (s2 - 2.0 * dm * s1) + n * (dm * dm);
-          a_std += sqrt(mm2 > 0.0 ? mm2 / (n - 1) : 0.0);
+          const double mm2 = (s2 - 2.0 * dm * s1) + dn * (dm * dm);
+          a_std += sqrt(mm2 > 0.0 ? mm2 / (dn - 1.0) : 0.0);
           const double e = mean - S;
           a_m += e;
           a_m2 = __builtin_fma(e, e, a_m2);
-          const double yl = my[(rc + rem - 1) * kDimTile + dl] - sh;   // lag n - 1: (x[n-1] - x[0])^2
+          const double yl = my[(rc + rem - 1) * kDimTile + lane_id()] - sh;   // lag n - 1: (x[n-1] - x[0])^2
           a_last = __builtin_fma(yl, yl, a_last);
         }
       }
