@@ -463,7 +463,7 @@ hmc_status hmc_stream_accumulate(const double* window, int64_t n_chains, int64_t
   if (!window || !shift || !s1 || !s2 || !work || !vsum || n_chains < 1 || D < 1 || rows < 0 || carry < 0 ||
       n_half < 2 || pos0 < 0 || wrap < 1 || slot0 < 0 || slot0 >= wrap || carry + rows > wrap)
     return fail(HMC_EINVAL, "bad arguments");
-  if (tmax != 8 && tmax != 16 && tmax != 32 && tmax != 64) return fail(HMC_EINVAL, "tmax must be 8, 16, 32, 48 or 64");
+  if (tmax != 8 && tmax != 16 && tmax != 32 && tmax != 64) return fail(HMC_EINVAL, "tmax must be 8, 16, 32 or 64");
   if (carry < (pos0 < tmax ? pos0 : tmax)) return fail(HMC_EINVAL, "carry must be >= min(tmax, pos0)");
   if (rows == 0) return HMC_OK;
   return hip_status(hmc::launch_stream_accum(window, n_chains, chain_stride, sample_stride, D, wrap, slot0, carry, rows,
