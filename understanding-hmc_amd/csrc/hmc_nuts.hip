@@ -120,7 +120,15 @@ __device__ __forceinline__ int nuts_nvec(int d_max) { return V_SLOTS + 2 * (d_ma
 
 // bytes of the work queue block, zeroed before every launch: head, a spare word, done[n] (u32),
 // padded to a multiple of 16
-inline size_t nuts_queue_bytes(int64_t n) { return (size_t)((16 + 4 * n + 15) / 16 * 16); }
+__host__ __device__ inline size_t nuts_queue_bytes(int64_t n) { return (size_t)((16 + 4 * n + 15) / 16 * 16); }
+
+// Philox momenta are drawn ahead of the tree kernel (k_nuts_momenta) for up to kNutsMomIters
+// iterations per launch into the workspace tail: a tree start then costs a 16-byte load per lane
+// pair, issued with the chain's state loads, instead of ~23k clocks of Philox + Box-Muller that
+// the whole wave waited for at every tree end (profiles/r03_c5_nuts_phases.json), and the tree
+// kernel needs no Box-Muller tables in LDS.  Longer ranges run as several launches.
+constexpr int kNutsMomIters = 32;
+__host__ __device__ inline int64_t nuts_mom_doubles(int64_t n, int MT) { return n * kNutsMomIters * 4 * MT * 4; }
 
 // Workspace: per chain slot, nvec vectors of Dp = 4M doubles (dims, zero padded), slot-contiguous,
 // the 16 slots of a wave in one block addressed through a wave-uniform buffer descriptor (SGPR
@@ -242,6 +250,40 @@ __device__ __forceinline__ double mac(double acc, double x, double y) {
   else return __builtin_fma(x, y, acc);
 }
 
+// Momenta of iterations [it0, it1) (it1 - it0 <= kNutsMomIters) for every chain: p ~ N(0, cov_p)
+// with a diagonal cov_p (samplers.py:565, :829), exactly the tree kernel's former in-kernel draws
+// (pair slot h + 4m -> dims h + 4m and h + 4m + 4, table Box-Muller, pscale, zero padding).
+// Layout: per (chain, iteration) one 4M-double vector in the workspace's pair layout (ws_elem):
+// 16-byte slot s = 4j + h holds dims (h + 8j, h + 8j + 4), so slot s sits at doubles 2s..2s+1 and
+// consecutive threads write consecutive 16-byte slots.
+template <int MT, bool GEN>
+__global__ __launch_bounds__(256) void k_nuts_momenta(RandArgs a, double* __restrict__ pm) {
+  constexpr int M = 4 * MT;
+  __shared__ double s_ntab[kNormalTableDoubles];
+  init_normal_tables(s_ntab);
+  __syncthreads();
+  const int K = a.it1 - a.it0;
+  const int64_t total = a.n * K * (2 * M);
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < total; s += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t vec = s / (2 * M);
+    const int r = (int)(s - vec * (2 * M));
+    const int64_t c = vec / K;
+    const int it = a.it0 + (int)(vec - c * K);
+    const int h = r & 3, m = 2 * (r >> 2);
+    double z0, z1;
+    normal_pair_tab(draw_block((uint32_t)(h + 4 * m), (uint32_t)it, (uint64_t)(a.chain_offset + c), a.k0, a.k1),
+                    s_ntab, z0, z1);
+    const int d0 = h + 4 * m, d1 = d0 + 4;
+    if (GEN && a.pscale) {
+      z0 *= a.pscale[min(d0, a.D - 1)];
+      z1 *= a.pscale[min(d1, a.D - 1)];
+    }
+    z0 = d0 < a.D ? z0 : 0.0;
+    z1 = d1 < a.D ? z1 : 0.0;
+    *reinterpret_cast<double2*>(pm + (c * kNutsMomIters + (vec - c * K)) * (4 * M) + 2 * r) = make_double2(z0, z1);
+  }
+}
+
 // MASS: full (non-diagonal) cov_p (implies GEN): LDS holds the kick matrix inv(cov_p).P
 // (stage_precision), p = C z, and every energy takes P x and inv(cov_p) p from two L2 products
 // (matvec_global) in converged code.  Its own instantiation, like the dense Random kernel's.
@@ -251,9 +293,12 @@ template <int MT, bool EXACT, bool GEN, bool REPLAY, bool MASS = false, int SHOR
 __global__ __launch_bounds__(64 * kNutsWaves) __attribute__((amdgpu_waves_per_eu(kNutsWaves / 4, kNutsWaves / 4)))
 void k_nuts_iters(RandArgs a) {
   constexpr int M = 4 * MT;
+  // PG: Philox momenta drawn ahead by k_nuts_momenta (all but the dense-mass instances, whose
+  // p = C z needs the tile's MFMA product and keeps the in-kernel draws and their tables)
+  constexpr bool PG = !REPLAY && !MASS;
   extern __shared__ double sP[];
-  __shared__ double s_ntab[REPLAY ? 2 : kNormalTableDoubles];   // Box–Muller tables (Philox momentum)
-  if constexpr (!REPLAY) init_normal_tables(s_ntab);             // synchronised by stage_precision
+  __shared__ double s_ntab[(REPLAY || PG) ? 2 : kNormalTableDoubles];   // Box–Muller tables (MASS momentum)
+  if constexpr (!REPLAY && !PG) init_normal_tables(s_ntab);             // synchronised by stage_precision
   stage_precision<MT, SHORT>(a, sP);
 
   const int lane = threadIdx.x & (kWave - 1);
@@ -272,6 +317,7 @@ void k_nuts_iters(RandArgs a) {
   int64_t* const tcur = reinterpret_cast<int64_t*>(a.ws + n_waves * wave_doubles);
   unsigned long long* const queue = reinterpret_cast<unsigned long long*>(tcur + n_waves * 16);   // zeroed per launch
   unsigned* const done = reinterpret_cast<unsigned*>(queue + 2);    // per chain: iterations done (zeroed per launch)
+  const double* const pm = reinterpret_cast<const double*>(queue) + nuts_queue_bytes(a.n) / 8;   // k_nuts_momenta
   const unsigned long long n_units = (unsigned long long)a.n * (unsigned long long)(a.it1 - a.it0);
   unsigned waited = 0;
   int64_t c = 0;
@@ -399,6 +445,15 @@ void k_nuts_iters(RandArgs a) {
           }
           Eprev = ld_wt_d(a.Eprev + c);
           tpos = REPLAY ? ld_wt(tcur + c) : 0;
+          if constexpr (PG) {                           // this iteration's momentum, with the state
+            const double* pv = pm + (c * kNutsMomIters + (it - a.it0)) * (4 * M) + 2 * h;
+#pragma unroll
+            for (int m = 0; m < M; m += 2) {
+              const double2 z = *reinterpret_cast<const double2*>(pv + 4 * m);
+              p[m] = z.x;
+              p[m + 1] = z.y;
+            }
+          }
           state = S_GRAD;                               // gradient at q in the next wave step
         }
       }
@@ -416,6 +471,15 @@ void k_nuts_iters(RandArgs a) {
             kin += z * (dim_minv<MT, GEN>(a, h + 4 * m) * z);
             vput<M>(W, V_RIGHT_P, m, z);
             vput<M>(W, V_LEFT_P, m, -z);
+          }
+        } else if constexpr (PG) {                     // p loaded with the chain's state (S_WAIT)
+#pragma unroll
+          for (int m = 0; m < M; m += 2) {
+            const double z0 = p[m], z1 = p[m + 1];
+            kin += z0 * (dim_minv<MT, GEN>(a, h + 4 * m) * z0);
+            kin += z1 * (dim_minv<MT, GEN>(a, h + 4 * m + 4) * z1);
+            vput2<M>(W, V_RIGHT_P, m, z0, z1);
+            vput2<M>(W, V_LEFT_P, m, -z0, -z1);
           }
         } else {
 #pragma unroll
@@ -634,67 +698,6 @@ void k_nuts_iters(RandArgs a) {
     // check points of mpt, incrementally (cp_point): mpt - r + 1, then + r/2, + r/4, ...
     int cp_half = checking ? cp_r(mpt) : 2;
     int cp_pt = mpt - cp_half + 1;
-#ifdef HMC_NUTS_CHECK_PAIRS
-    // A/B variant: two check points per pass (their four vectors in flight together: one memory
-    // round trip per pair); a rejection by either is the reference's outcome (checks have no side
-    // effects, so evaluating the second after a rejecting first changes nothing)
-    for (int ci = 0; ci < ncheck_w; ci += 2) {
-      const bool doit0 = alive_chk && ci < ncheck, doit1 = alive_chk && ci + 1 < ncheck;
-      if (ci > 0) {
-        cp_half >>= 1;
-        cp_pt += cp_half;
-      }
-      const int l0 = doit0 ? cp_pt : 1;
-      const int cp_half1 = cp_half >> 1;
-      const int l1 = doit1 ? cp_pt + cp_half1 : 1;
-      if (ci + 1 < ncheck_w) {
-        cp_half = cp_half1;
-        cp_pt += cp_half1;
-      }
-      const int s0 = save_slot(l0, a.d_max), s1 = save_slot(l1, a.d_max);
-      double r0 = 0.0, l0d = 0.0, r1 = 0.0, l1d = 0.0;
-      if (doit0 || doit1) {
-        double qa[M], pa[M], qb[M], pb[M];
-        if (doit0) {
-          vload<M>(W, V_SLOTS, 2 * s0, qa);
-          vload<M>(W, V_SLOTS + 1, 2 * s0, pa);
-        }
-        if (doit1) {
-          vload<M>(W, V_SLOTS, 2 * s1, qb);
-          vload<M>(W, V_SLOTS + 1, 2 * s1, pb);
-        }
-        double A0 = 0.0, B0 = 0.0, A1 = 0.0, B1 = 0.0;
-        if (doit0) {
-#pragma unroll
-          for (int m = 0; m < M; ++m) {
-            const double Dq = q[m] - qa[m];
-            A0 = mac<EXACT>(A0, Dq, p[m]);
-            B0 = mac<EXACT>(B0, Dq, pa[m]);
-          }
-        }
-        if (doit1) {
-#pragma unroll
-          for (int m = 0; m < M; ++m) {
-            const double Dq = q[m] - qb[m];
-            A1 = mac<EXACT>(A1, Dq, p[m]);
-            B1 = mac<EXACT>(B1, Dq, pb[m]);
-          }
-        }
-        r0 = udir == 0 ? A0 : B0;
-        l0d = udir == 0 ? B0 : A0;
-        r1 = udir == 0 ? A1 : B1;
-        l1d = udir == 0 ? B1 : A1;
-      }
-      r0 = chain_sum4(r0);
-      l0d = chain_sum4(l0d);
-      r1 = chain_sum4(r1);
-      l1d = chain_sum4(l1d);
-      if ((doit0 && l0d < 0.0 && r0 < 0.0) || (doit1 && l1d < 0.0 && r1 < 0.0)) {   // :727-732
-        reject = true;
-        alive_chk = false;
-      }
-    }
-#else
     for (int ci = 0; ci < ncheck_w; ++ci) {
       const bool doit = alive_chk && ci < ncheck;
       if (ci > 0) {
@@ -731,7 +734,6 @@ void k_nuts_iters(RandArgs a) {
         }                                               // (release, :735-736: nothing to free)
       }
     }
-#endif
     NUTS_PHASE(5);
     if (later && !reject) {                             // progressive sampling (:743-751)
       const double E_max_prev = E_max_now;
@@ -763,6 +765,12 @@ void k_nuts_iters(RandArgs a) {
       double oqv[M], opv[M];
       d4 og[MT];
       const int b = udir == 0 ? V_RIGHT_Q : V_LEFT_Q;    // this end <- (q, p)
+      const int o = udir == 0 ? V_LEFT_Q : V_RIGHT_Q;   // the other end
+      // the other end's loads first: the stores behind them in the in-order vmcnt queue do not
+      // delay the wait for the loads (b != o, so the order changes nothing else)
+      vload<M>(W, 0, o, oqv);
+      vload<M>(W, 1, o, opv);
+      gload<MT>(W, 2, o, og);
       vstore<M>(W, 0, b, q);
       vstore<M>(W, 1, b, p);
       gstore<MT>(W, 2, b, acc);
@@ -775,10 +783,6 @@ void k_nuts_iters(RandArgs a) {
         old2 = 2 - old2;
         maha_old = maha_new;
       }
-      const int o = udir == 0 ? V_LEFT_Q : V_RIGHT_Q;   // the other end
-      vload<M>(W, 0, o, oqv);
-      vload<M>(W, 1, o, opv);
-      gload<MT>(W, 2, o, og);
       // A = (q - q_other).p, B = (q - q_other).p_other; (tr, tl) = (A, -B) forward, (-B, A)
       // backward: the reference's terms up to exact sign flips
       double tA = 0.0, tB = 0.0;
@@ -846,7 +850,34 @@ void k_nuts_iters(RandArgs a) {
 }
 
 template <int MT, bool EXACT>
+hipError_t launch_nuts_mt3(const RandArgs& args, bool gen, bool replay, hipStream_t s);
+
+// Launches of at most kNutsMomIters iterations, each after its momenta (Philox, diagonal cov_p).
+template <int MT, bool EXACT>
 hipError_t launch_nuts_mt2(const RandArgs& args, bool gen, bool replay, hipStream_t s) {
+  if (replay || args.minvf) return launch_nuts_mt3<MT, EXACT>(args, gen, replay, s);
+  const int64_t n_waves = (args.n + 15) / 16;
+  const int64_t wave_doubles = (int64_t)(V_SLOTS + 2 * (args.d_max + 1)) * 4 * MT * kWave;
+  double* pm = args.ws + n_waves * wave_doubles + n_waves * 16 + nuts_queue_bytes(args.n) / 8;
+  for (int i0 = args.it0; i0 < args.it1; i0 += kNutsMomIters) {
+    RandArgs a = args;
+    a.it0 = i0;
+    a.it1 = std::min(args.it1, i0 + kNutsMomIters);
+    const int64_t slots = a.n * (a.it1 - a.it0) * (8 * MT);
+    const dim3 mgrid((unsigned)std::max<int64_t>(1, std::min<int64_t>((slots + 255) / 256, (int64_t)device_cus() * 8)));
+#ifndef HMC_NUTS_DEV_C5
+    if (gen) k_nuts_momenta<MT, true><<<mgrid, 256, 0, s>>>(a, pm);
+    else
+#endif
+      k_nuts_momenta<MT, false><<<mgrid, 256, 0, s>>>(a, pm);
+    if (hipError_t e = hipGetLastError()) return e;
+    if (hipError_t e = launch_nuts_mt3<MT, EXACT>(a, gen, replay, s)) return e;
+  }
+  return hipSuccess;
+}
+
+template <int MT, bool EXACT>
+hipError_t launch_nuts_mt3(const RandArgs& args, bool gen, bool replay, hipStream_t s) {
   RandArgs a = args;
   // persistent: one block per CU (LDS: P + index tables), chains handed out by the queue
   const int64_t blocks = (a.n + 16 * kNutsWaves - 1) / (16 * kNutsWaves);
@@ -857,6 +888,10 @@ hipError_t launch_nuts_mt2(const RandArgs& args, bool gen, bool replay, hipStrea
   if (hipError_t e = hipMemsetAsync(queue, 0, nuts_queue_bytes(a.n), s)) return e;
   a.wait_cap = nuts_wait_cap((int64_t)grid.x * kNutsWaves * 16, a.n, a.d_max);
   const size_t lds = (size_t)MT * 4 * MT * kWave * sizeof(double);
+#ifdef HMC_NUTS_DEV_C5
+  if constexpr (MT == 7 && !EXACT) k_nuts_iters<MT, EXACT, false, false, false, kShortAlways><<<grid, 64 * kNutsWaves, lds, s>>>(a);
+  return hipGetLastError();
+#endif
   if (a.minvf) {
     if (replay) k_nuts_iters<MT, EXACT, true, true, true><<<grid, 64 * kNutsWaves, lds, s>>>(a);
     else k_nuts_iters<MT, EXACT, true, false, true><<<grid, 64 * kNutsWaves, lds, s>>>(a);
@@ -890,10 +925,16 @@ hipError_t launch_nuts_mt(const RandArgs& a, bool exact, bool gen, bool replay, 
 int64_t nuts_ws_doubles(int64_t n, int D, int d_max) {
   const int MT = dense_tiles(D);
   const int64_t waves = (n + 15) / 16;
-  // vectors + tape cursors + work queue (head, spare, per-chain iterations done)
-  return waves * (int64_t)(V_SLOTS + 2 * (d_max + 1)) * 4 * MT * kWave + waves * 16 + nuts_queue_bytes(n) / 8;
+  // vectors + tape cursors + work queue (head, spare, per-chain iterations done) + momenta
+  return waves * (int64_t)(V_SLOTS + 2 * (d_max + 1)) * 4 * MT * kWave + waves * 16 + nuts_queue_bytes(n) / 8 +
+         nuts_mom_doubles(n, MT);
 }
 
+#ifdef HMC_NUTS_DEV_C5
+// dev-only build of the c5 instance alone (seconds instead of minutes per A/B compile): objdump /
+// register checks; not a usable library
+hipError_t launch_nuts_iters(const RandArgs& a, bool, bool, hipStream_t s) { return launch_nuts_mt2<7, false>(a, false, false, s); }
+#else
 hipError_t launch_nuts_iters(const RandArgs& a, bool exact, bool replay, hipStream_t s) {
   const bool gen = a.q0 || a.minv || a.pscale || a.dtv || a.minvf;
   switch (dense_tiles(a.D)) {
@@ -905,5 +946,6 @@ hipError_t launch_nuts_iters(const RandArgs& a, bool exact, bool replay, hipStre
   }
   return hipErrorInvalidValue;
 }
+#endif
 
 }  // namespace hmc
