@@ -178,7 +178,8 @@ int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max);
  * resample -> E0 -> tree doubling until both ends U-turn (sub-tree U-turn checks against the
  * saved odd points, progressive sampling, biased sub-tree acceptance) -> store.
  * Replaces HMC_sampler.gen_sample_NUTS, samplers.py:563-791 (+ utils.py:222-385).
- * Dense precision only (pass diagonal targets as dense), D <= 128, 1 <= d_max <= 15.
+ * Dense precision only (pass diagonal targets as dense), any D, 1 <= d_max <= 15: D <= 128 runs
+ * the 16-chain MFMA tree kernel, D > 128 one wave per chain (diagonal cov_p only there).
  * `workspace` (hmc_nuts_workspace_size bytes) must be zeroed before the first call of a run
  * and kept between calls.  Counters: LEAPFROG (= ENERGY_EVALS), UNSTABLE (|E-E0| > 1000
  * rejections, :647), DMAX (chain-iterations that reached d_max; the reference aborts there,

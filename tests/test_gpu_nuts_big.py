@@ -1,0 +1,146 @@
+"""NUTS beyond the MFMA tree kernel's register budget (hmc_nuts_big.hip): dense targets with
+D > 128, which the reference's NUTS takes through np.dot at any D (samplers.py:495-808, :835-837).
+
+Replay mode vs the oracle (oracle/hmc_oracle.py restating gen_sample_NUTS) on the same momenta
+and the same per-chain tape of directions / uniforms: identical leapfrog and instability counts,
+q_chain within 1e-9, E within 1e-10 relative (GEMV sums in k order vs BLAS).  Philox mode: the
+stationary law, determinism and shard invariance (draws keyed by the global chain id)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import hmc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+class FastMVN(O.MVNTarget):
+    """V = 0.5 (logdet const + x.P.x) instead of scipy's eigh-based logpdf (same value to ~1e-14)."""
+
+    def __init__(self, q0, cov0):
+        super().__init__(q0, cov0)
+        D = self.q0.size
+        self.c = D * np.log(2 * np.pi) + np.linalg.slogdet(self.cov0)[1]
+
+    def V(self, q):
+        x = q - self.q0
+        return 0.5 * (self.c + x @ (self.inv_cov0 @ x))
+
+
+CASES = [
+    # D, rho, q0 scale, Nchain, Niter, wu, thin, dt, d_max, diag cov_p, dt vector, on_dmax
+    (136, 0.9, 0.0, 3, 10, 1, 1, 0.1, 9, False, False, "raise"),
+    (300, 0.5, 0.5, 2, 4, 0, 2, 0.15, 8, True, True, "break"),
+    (160, 0.99, 0.0, 3, 4, 0, 1, 0.9, 6, False, False, "break"),     # large dt: |E - E0| > 1000 guard
+    (129, 0.3, 0.0, 5, 6, 2, 1, 0.02, 3, False, False, "break"),     # d_max reached every iteration
+]
+
+
+def _case(case):
+    D, rho, qs, N, Niter, wu, thin, dt, d_max, diag_p, dtvec, on_dmax = case
+    rs = np.random.RandomState(2000 + D)
+    cov = O.mvn_cov(D, rho) if rho > 0 else np.eye(D)
+    q0 = rs.standard_normal(D) * qs
+    cov_p = np.diag(rs.uniform(0.5, 2.0, D)) if diag_p else None
+    dts = rs.uniform(0.5, 1.0, D) * dt if dtvec else dt
+    q_start = q0 + rs.standard_normal((N, D)) * 1.2
+    scale = np.sqrt(np.diag(cov_p)) if diag_p else np.ones(D)
+    p0 = rs.standard_normal((N, D)) * scale
+    P = rs.standard_normal((N, Niter, D)) * scale
+    tape = rs.uniform(0.0, 2.0, (N, Niter * 2 * (2 ** d_max + d_max + 2)))   # int(v) = direction, v = uniform
+    return cov, q0, cov_p, dts, q_start, p0, P, tape
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"D{c[0]}_rho{c[1]}_dt{c[7]}_dmax{c[8]}" for c in CASES])
+@pytest.mark.parametrize("fp_mode", ["exact", "fast"])
+def test_nuts_large_D_vs_oracle(case, fp_mode):
+    from hmc_amd import _lib as H
+    from hmc_amd.engine import NutsEngine
+    from hmc_amd.target import MVNTarget
+    D, rho, qs, N, Niter, wu, thin, dt, d_max, diag_p, dtvec, on_dmax = case
+    cov, q0, cov_p, dts, q_start, p0, P, tape = _case(case)
+    tgt = FastMVN(q0, cov)
+    ref = O.gen_sample_nuts(O.HMCCore(tgt, dts, cov_p), q_start, N, Niter, wu, thin, d_max,
+                            O.ReplayDraws(p0, P, tape=tape.copy()), on_dmax=on_dmax)
+    eng = NutsEngine(MVNTarget(q0, cov, logdet_const=tgt.c), N, Niter, wu, thin, d_max, dts, cov_p=cov_p,
+                     rng="replay", fp_mode=fp_mode, on_dmax=on_dmax)
+    eng.set_replay(p0, P, tape)
+    eng.init(q_start)
+    eng.run(1, 3)                                 # two launches: the tape cursors persist between them
+    eng.run(3, Niter + 1)
+    torch.cuda.synchronize()
+    c = eng.read_counters()
+    assert int(c[H.CNT_OOB_REJECT]) == 0
+    assert int(c[H.CNT_LEAPFROG]) == ref["n_leapfrog"]
+    assert int(c[H.CNT_UNSTABLE]) == ref["n_unstable"]
+    if on_dmax == "raise":
+        assert int(c[H.CNT_DMAX]) == 0
+    np.testing.assert_allclose(eng.q_chain.cpu().numpy(), ref["q_chain"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(eng.E_chain.cpu().numpy(), ref["E_chain"], rtol=1e-10, atol=1e-10)
+    np.testing.assert_allclose(eng.dE_chain.cpu().numpy(), ref["dE_chain"], rtol=1e-8, atol=1e-9)
+    if case[0] == 160:
+        assert ref["n_unstable"] > 0              # the case exercises the guard
+    if case[0] == 129:
+        assert int(c[H.CNT_DMAX]) == N * Niter    # and this one the d_max break
+
+
+def test_nuts_large_D_through_sampler():
+    """The drop-in surface: HMC_sampler(sampler_type='NUTS') at D = 200 with the reference's
+    accounting (N_total_steps, accept_R = 1) on replayed draws vs the oracle."""
+    from hmc_amd.samplers import HMC_sampler
+    from hmc_amd.target import MVNTarget
+    D, N, Niter, wu, d_max, dt = 200, 2, 4, 1, 8, 0.1
+    rs = np.random.RandomState(5)
+    cov = O.mvn_cov(D, 0.8)
+    q_start = rs.standard_normal((N, D))
+    p0, P = rs.standard_normal((N, D)), rs.standard_normal((N, Niter, D))
+    tape = rs.uniform(0.0, 2.0, (N, Niter * 2 * (2 ** d_max + d_max + 2)))
+    tgt = FastMVN(np.zeros(D), cov)
+    ref = O.gen_sample_nuts(O.HMCCore(tgt, dt), q_start, N, Niter, wu, 1, d_max,
+                            O.ReplayDraws(p0, P, tape=tape.copy()))
+    h = HMC_sampler(D, None, None, Nchain=N, Niter=Niter, thin_rate=1, warm_up_num=wu, sampler_type="NUTS",
+                    dt=dt, d_max=d_max, target=MVNTarget(np.zeros(D), cov, logdet_const=tgt.c), rng="replay")
+    h.set_nuts_replay(p0, P, tape)
+    h.gen_sample(q_start, verbose=False)
+    assert h.n_leapfrog == ref["n_leapfrog"]
+    assert h.N_total_steps == ref["N_total_steps"]
+    assert h.accept_R == 1.0
+    np.testing.assert_allclose(h.q_chain, ref["q_chain"], rtol=1e-9, atol=1e-9)
+
+
+def test_nuts_large_D_philox_stationary_and_shards():
+    """Chains started in N(0, Sigma) stay there (per-dim variance 1, corr rho); runs repeat bit for
+    bit, and two shards (chain_offset) reproduce the one-batch run (Philox keyed by global chain)."""
+    from hmc_amd.engine import NutsEngine
+    from hmc_amd.target import MVNTarget
+    D, rho, N, Niter = 160, 0.6, 1024, 3
+    cov = O.mvn_cov(D, rho)
+    qs = np.random.RandomState(4).standard_normal((N, D)) @ np.linalg.cholesky(cov).T
+    tgt = MVNTarget(np.zeros(D), cov)
+
+    def run(lo, hi):
+        e = NutsEngine(tgt, hi - lo, Niter, 1, 1, 10, 0.2, rng="philox", seed=11, chain_offset=lo,
+                       on_dmax="break")
+        e.init(qs[lo:hi])
+        e.run(1, Niter + 1)
+        torch.cuda.synchronize()
+        return e.q_chain.cpu().numpy(), e.read_counters()
+    qc, cnt = run(0, N)
+    last = qc[:, -1, :]
+    assert np.abs(last.var(axis=0).mean() - 1) < 6 * np.sqrt(2 / (N * D)) + 0.02
+    assert abs(np.corrcoef(last[:, 0], last[:, 1])[0, 1] - rho) < 6 * (1 - rho ** 2) / np.sqrt(N) + 0.02
+    assert np.isfinite(qc).all()
+    assert np.array_equal(qc, run(0, N)[0])
+    a, b = run(0, 400), run(400, N)
+    assert np.array_equal(np.concatenate([a[0], b[0]]), qc)
+    assert (a[1] + b[1] == cnt).all()
+
+
+def test_nuts_large_D_full_cov_p_raises():
+    """A full (non-diagonal) cov_p stays limited to D <= 128 for NUTS: NotImplementedError, no launch."""
+    from hmc_amd.engine import NutsEngine
+    from hmc_amd.target import MVNTarget
+    D = 136
+    with pytest.raises(NotImplementedError):
+        NutsEngine(MVNTarget(np.zeros(D), O.mvn_cov(D, 0.5)), 2, 4, 0, 1, 6, 0.1, rng="philox",
+                   cov_p=O.mvn_cov(D, 0.3))

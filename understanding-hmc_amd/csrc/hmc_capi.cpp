@@ -306,7 +306,8 @@ int64_t hmc_random_workspace_size(const hmc_target* t, int64_t n_chains) {
 }
 
 int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max) {
-  if (D < 1 || n_chains < 0 || d_max < 1 || d_max > 15 || !hmc::dense_tiles(D)) return 0;
+  if (D < 1 || n_chains < 0 || d_max < 1 || d_max > 15) return 0;
+  if (!hmc::dense_tiles(D)) return hmc::nuts_big_ws_doubles(n_chains, D, d_max) * (int64_t)sizeof(double);
   return hmc::nuts_ws_doubles(n_chains, D, d_max) * (int64_t)sizeof(double);
 }
 
@@ -322,7 +323,8 @@ hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_s
   if (s->d_max < 1 || s->d_max > 15) return fail(HMC_EINVAL, "d_max must be in [1, 15]");
   if (hmc_status e = check_mass(t, k, s)) return e;
   if (t->kind != HMC_TARGET_DENSE) return fail(HMC_ENOTSUP, "NUTS runs the dense kernel: pass prec as dense");
-  if (!hmc::dense_tiles(t->D)) return fail(HMC_ENOTSUP, "dense target: D=%d > 128 not supported", t->D);
+  const bool big = !hmc::dense_tiles(t->D);   // D > 128: hmc_nuts_big.hip
+  if (big && k->minv_full) return fail(HMC_ENOTSUP, "NUTS with a full cov_p and D=%d: not supported", t->D);
   const bool replay = s->rng_mode == HMC_RNG_REPLAY;
   if (replay && (!r || !r->p || !r->tape || r->tape_stride < 1)) return fail(HMC_EINVAL, "replay mode needs p and tape");
   if (s->n_chains == 0 || s->iter_end == s->iter_begin) return HMC_OK;
@@ -338,6 +340,8 @@ hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_s
   }
   a.traj_q = nullptr;
   a.n_save = 0;
+  if (big) return hip_status(hmc::launch_nuts_big(a, s->fp_mode == HMC_MODE_EXACT, replay, (hipStream_t)stream),
+                             "hmc_nuts_iters(large D)");
   return hip_status(hmc::launch_nuts_iters(a, s->fp_mode == HMC_MODE_EXACT, replay, (hipStream_t)stream),
                     "hmc_nuts_iters");
 }

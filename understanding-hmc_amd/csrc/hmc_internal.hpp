@@ -70,6 +70,9 @@ using DenseArgs = RandArgs;
 int dense_tiles(int D);
 int64_t nuts_ws_doubles(int64_t n, int D, int d_max);
 hipError_t launch_nuts_iters(const RandArgs& a, bool exact, bool replay, hipStream_t s);
+// NUTS for dense D > 128 (hmc_nuts_big.hip): one wave per chain, tree vectors in the workspace.
+int64_t nuts_big_ws_doubles(int64_t n, int D, int d_max);
+hipError_t launch_nuts_big(const RandArgs& a, bool exact, bool replay, hipStream_t s);
 
 Layout choose_layout(int D, int L_low, int L_high);
 

@@ -268,10 +268,11 @@ class NutsEngine(RandomEngine):
         assert on_dmax in ("raise", "break")
         self.d_max = int(d_max)
         self.on_dmax = 0 if on_dmax == "raise" else 1
+        if self.D > 128 and self._minv_full is not None:
+            raise NotImplementedError("NUTS with a full cov_p: D=%d not supported (D <= 128)" % self.D)
         nbytes = H.lib().hmc_nuts_workspace_size(self.D, self.N, self.d_max)
         if nbytes <= 0:
-            raise NotImplementedError("NUTS kernel: D=%d / d_max=%d not supported (D <= 128, 1 <= d_max <= 15)"
-                                      % (self.D, self.d_max))
+            raise NotImplementedError("NUTS kernel: d_max=%d not supported (1 <= d_max <= 15)" % self.d_max)
         self.ws = torch.zeros((nbytes + 7) // 8, dtype=torch.float64, device=self.device)
 
     def set_replay(self, p0, P, tape):
