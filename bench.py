@@ -412,6 +412,11 @@ def main():
     for _ in range(W):
         step(it)
         it += S
+    if window is not None and not a.no_ess and W > 0 and N >= 2:
+        # warm-up of the post-run diagnostics too: the first launch of their kernels loads the code
+        # object (~70 ms once per process); a 64-chain slice of the window has the same rows, so
+        # the same lag-kernel instance (conv_tmax depends on the rows only).  Results discarded.
+        convergence_stats(window[:min(N, 64)], warm_up_num=0, thin_rate=1)
     torch.cuda.synchronize(dev)
     c0 = eng.read_counters()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
