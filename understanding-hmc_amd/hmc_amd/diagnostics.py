@@ -110,7 +110,6 @@ def convergence_sums(sp, tmax):
 
 
 _TMAX = (8, 16, 32, 48, 64)
-_TMAX_FIRST = 16   # lags of the first pass (the full width only where a dimension needs more)
 
 
 def conv_tmax(n):
@@ -121,11 +120,20 @@ def conv_tmax(n):
     return next((t for t in _TMAX if t >= n - 2), _TMAX[-1])
 
 
-def _one_pass(sp, tmax, group):
-    """hmc_convergence_sums with lags 1..tmax, the two all-reduce rounds and R-hat: returns
-    (R device tensor, var numpy, Vt numpy (T, D) of lags 1..T, m)."""
+def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
+    """utils.py:77-159 on the GPU.  q_chain: (Nchain, Niter, D) NumPy array or CUDA tensor
+    (views such as q_chain_device[:, 1:, :] are read in place).  Returns (R, n_eff) NumPy.
+
+    One pass over the samples gives every per-dimension sum R-hat needs and the variogram of every
+    lag t < n up to 64, and of lag n - 1 (hmc_convergence_sums); the ESS termination
+    (utils.py:130-157) runs vectorised over the dimensions on the host, and only dimensions whose
+    criterion has not fired by then (n > 66 and slow mixing) read further lag blocks
+    (hmc_variogram).  Ranks all-reduce the per-dimension sums: two rounds, B needs the global
+    mean."""
+    sp = _Split(q_chain, thin_rate, warm_up_num)
     n, D = sp.n, sp.D
     dev = sp.t.device
+    tmax = conv_tmax(n)
     sums = convergence_sums(sp, tmax)
     S = sp.t.reshape(-1)[sp.base:sp.base + D].to(torch.float64)          # the kernels' shift S_d
     m_loc = 2 * sp.Nchain
@@ -144,41 +152,15 @@ def _one_pass(sp, tmax, group):
     var = W * (n - 1) / float(n) + B / float(n)                         # :123
     R = torch.sqrt(var / W)                                             # :126
     v = r1[2:3 + tmax].cpu().numpy()                                    # lags 1..tmax, then lag n - 1
+    var_h = var.cpu().numpy()
+    # ---- ESS (utils.py:128-157), vectorised over dims; more lags only where still undecided
     lmax = max(n - 1, 2)                                                # lags t < n exist
     T = min(tmax, lmax)
     v = np.vstack([v[:T], v[tmax:tmax + 1]]) if T == n - 2 else v[:T]  # + lag n - 1: complete
     T = v.shape[0]
     Vt = v / (m * (n - np.arange(1, T + 1)))[:, None]                   # utils.py:177
-    return R, var.cpu().numpy(), Vt, m
-
-
-def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
-    """utils.py:77-159 on the GPU.  q_chain: (Nchain, Niter, D) NumPy array or CUDA tensor
-    (views such as q_chain_device[:, 1:, :] are read in place).  Returns (R, n_eff) NumPy.
-
-    One pass over the samples gives every per-dimension sum R-hat needs and the variogram of lags
-    1..16 (hmc_convergence_sums); the ESS termination (utils.py:130-157) runs vectorised over the
-    dimensions on the host.  Well-mixed chains decide within those lags (the kernel's cost grows
-    with the lag count: 28.5 / 46 / 62 ms for 16 / 32 / 48 lags on the bench window).  If more
-    than a quarter of the dimensions have not decided (slow mixing), the pass is repeated once at
-    the full width: every lag t < n up to 64, and lag n - 1.  Dimensions still undecided then (a
-    few, or n > 66 and slow mixing) read further lag blocks (hmc_variogram) on a gathered copy of
-    their columns.  Ranks all-reduce the per-dimension sums: two rounds, B
-    needs the global mean; `need` comes from all-reduced sums, so every rank takes the same path."""
-    sp = _Split(q_chain, thin_rate, warm_up_num)
-    n, D = sp.n, sp.D
-    dev = sp.t.device
-    lmax = max(n - 1, 2)
-    tmax = conv_tmax(n)
-    first = min(tmax, _TMAX_FIRST)
-    for tm in ([first] if first == tmax else [first, tmax]):
-        R, var_h, Vt, m = _one_pass(sp, tm, group)
-        n_eff, need = ess_vectorised(Vt, var_h, n, m, complete=Vt.shape[0] >= lmax)
-        if 4 * int(need.sum()) <= D:             # none, or few: the gathered-dims blocks finish them
-            break
-    T = Vt.shape[0]
-    tmax = tm
-    LAST_INFO.update(tmax=tmax, lags=T, fallback_dims=int(need.sum()), fallback_passes=0, first_tmax=first)
+    n_eff, need = ess_vectorised(Vt, var_h, n, m, complete=T >= lmax)
+    LAST_INFO.update(tmax=tmax, lags=T, fallback_dims=int(need.sum()), fallback_passes=0)
     if need.any():
         # the dims whose criterion reads lags > T: gather their columns once (one strided read of
         # the lines holding them) into a compact (N, 2n, k) copy, and run the lag blocks on it (the
