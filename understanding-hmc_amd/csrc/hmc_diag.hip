@@ -409,21 +409,22 @@ __global__ __launch_bounds__(64 * conv_waves(G), conv_wpe(TW, G)) void k_conv_ld
       const bool hwin = cc * TW == gofs;          // this chunk's running S2 gives H_t of our lags
       const bool dly = cc * TW >= gofs;           // the delayed rows exist (gofs is a multiple of TW)
       const int isuf = pos_suf - cc * TW;         // suffix mark (T_t terms), if inside this chunk
-      auto rows = [&](auto plain_c, auto mom_c) {
+      auto rows = [&](auto plain_c, auto mom_c, auto dly_c) {
         constexpr bool PLAIN = decltype(plain_c)::value;   // whole chunk, no H_t / suffix event
         constexpr bool MOM = decltype(mom_c)::value;       // lag group 0 also sums the moments
+        constexpr bool DLY = decltype(dly_c)::value;       // the delayed rows exist (else: the shift)
         // rows one ahead: row i + 1's two LDS reads are issued before row i's FMAs, and no later
         // read moves above them (compiler fence), so at most two rows' values are live: a spill
         // reload here would wait for vmcnt(0), i.e. for the ring's in-flight loads
         const int ll = lane_id();                 // (recomputed: not worth a register)
         double xn = my[rc * kDimTile + ll];
-        double xdn = dly ? my[rd * kDimTile + ll] : sh;
+        double xdn = DLY ? my[rd * kDimTile + ll] : sh;
 #pragma unroll
         for (int i = 0; i < TW; ++i) {
           const double x = xn, xd = xdn;
           if (i + 1 < TW && (PLAIN || i + 1 < rem)) {
             xn = my[(rc + i + 1) * kDimTile + ll];
-            xdn = dly ? my[(rd + i + 1) * kDimTile + ll] : sh;
+            xdn = DLY ? my[(rd + i + 1) * kDimTile + ll] : sh;
           }
           asm volatile("" ::: "memory");
           if (PLAIN || i < rem) {
@@ -445,11 +446,18 @@ __global__ __launch_bounds__(64 * conv_waves(G), conv_wpe(TW, G)) void k_conv_ld
       };
       const bool plain = rem >= TW && !hwin && (isuf < 0 || isuf >= TW);
       if (g == 0) {
-        if (plain) rows(std::true_type{}, std::true_type{});
-        else rows(std::false_type{}, std::true_type{});
+        if (plain) rows(std::true_type{}, std::true_type{}, std::true_type{});   // g = 0: dly always
+        else rows(std::false_type{}, std::true_type{}, std::true_type{});
       } else {
-        if (plain) rows(std::true_type{}, std::false_type{});
-        else rows(std::false_type{}, std::false_type{});
+        // dly as a template argument: g is not wave-uniform to the compiler, so a runtime dly made
+        // every delayed read an exec-masked branch (a default move and mask saves per row)
+        if (dly) {
+          if (plain) rows(std::true_type{}, std::false_type{}, std::true_type{});
+          else rows(std::false_type{}, std::false_type{}, std::true_type{});
+        } else {
+          if (plain) rows(std::true_type{}, std::false_type{}, std::false_type{});
+          else rows(std::false_type{}, std::false_type{}, std::false_type{});
+        }
       }
       if (cc == nch - 1) {                        // the split chain is complete
         // q4 = 4 (S2 - S2 through n-1-gofs) + sum of the ring's (-2 y)^2: 4x the T_t suffix sums,
