@@ -144,3 +144,47 @@ def test_nuts_large_D_full_cov_p_raises():
     with pytest.raises(NotImplementedError):
         NutsEngine(MVNTarget(np.zeros(D), O.mvn_cov(D, 0.5)), 2, 4, 0, 1, 6, 0.1, rng="philox",
                    cov_p=O.mvn_cov(D, 0.3))
+
+
+def test_nuts_large_D_streaming_and_resume(tmp_path):
+    """The large-D NUTS path under the surface's streaming mode (HMC_sampler(store_chain=False):
+    E_chain identical to the stored run, R-hat equal to the oracle's convergence_stats on the stored
+    q_chain), and a checkpoint at iteration 7 resumed in a fresh engine: bit-identical to the
+    uninterrupted run (Philox keyed by iteration; the workspace travels in the checkpoint)."""
+    from hmc_amd.engine import NutsEngine
+    from hmc_amd.samplers import HMC_sampler
+    from hmc_amd.target import MVNTarget
+    D, N, Niter, wu = 144, 16, 40, 8
+    cov = O.mvn_cov(D, 0.5)
+    tgt = MVNTarget(np.zeros(D), cov)
+    q_start = np.random.RandomState(8).standard_normal((N, D))
+    kw = dict(Nchain=N, Niter=Niter, sampler_type="NUTS", dt=0.2, warm_up_num=wu, rng="philox", seed=5,
+              fp_mode="fast", iters_per_launch=8, target=tgt, d_max=10)
+    full = HMC_sampler(D, None, None, **kw)
+    full.gen_sample(q_start, verbose=False)
+    h = HMC_sampler(D, None, None, store_chain=False, stream_tmax=16, stream_feed=16, **kw)
+    h.gen_sample(q_start, verbose=False)
+    assert h.q_chain is None
+    assert np.array_equal(h.E_chain, full.E_chain)
+    h.compute_convergence_stats()
+    R_ref, _ = O.convergence_stats(full.q_chain[:, 1:, :], thin_rate=1, warm_up_num=0)
+    np.testing.assert_allclose(h.R_q, R_ref, rtol=1e-10)
+
+    def make():
+        return NutsEngine(tgt, N, 12, 2, 1, 10, 0.2, rng="philox", seed=3, on_dmax="break")
+    ref = make()
+    ref.init(q_start)
+    ref.run(1, 13)
+    a = make()
+    a.init(q_start)
+    a.run(1, 7)
+    path = str(tmp_path / "nuts_big.npz")
+    a.save(path, 7)
+    b = make()
+    it = b.restore(path)
+    assert it == 7
+    b.run(it, 13)
+    torch.cuda.synchronize()
+    assert torch.equal(b.q, ref.q)
+    assert torch.equal(b.q_chain, ref.q_chain)
+    np.testing.assert_array_equal(b.read_counters(), ref.read_counters())

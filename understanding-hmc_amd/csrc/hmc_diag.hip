@@ -409,10 +409,11 @@ __global__ __launch_bounds__(64 * conv_waves(G), conv_wpe(TW, G)) void k_conv_ld
       const bool hwin = cc * TW == gofs;          // this chunk's running S2 gives H_t of our lags
       const bool dly = cc * TW >= gofs;           // the delayed rows exist (gofs is a multiple of TW)
       const int isuf = pos_suf - cc * TW;         // suffix mark (T_t terms), if inside this chunk
-      auto rows = [&](auto plain_c, auto mom_c, auto dly_c) {
+      auto rows = [&](auto plain_c, auto mom_c, auto dly_c, auto ev_c) {
         constexpr bool PLAIN = decltype(plain_c)::value;   // whole chunk, no H_t / suffix event
         constexpr bool MOM = decltype(mom_c)::value;       // lag group 0 also sums the moments
         constexpr bool DLY = decltype(dly_c)::value;       // the delayed rows exist (else: the shift)
+        constexpr int EV = decltype(ev_c)::value;          // events in this chunk: 1 H_t, 2 suffix mark
         // rows one ahead: row i + 1's two LDS reads are issued before row i's FMAs, and no later
         // read moves above them (compiler fence), so at most two rows' values are live: a spill
         // reload here would wait for vmcnt(0), i.e. for the ring's in-flight loads
@@ -436,29 +437,30 @@ __global__ __launch_bounds__(64 * conv_waves(G), conv_wpe(TW, G)) void k_conv_ld
             s2 = __builtin_fma(y, y, s2);
 #pragma unroll
             for (int k = 0; k < TW; ++k) v[k] = __builtin_fma(y, ring[(i - 1 - k) & (TW - 1)], v[k]);
-            if (!PLAIN) {
-              if (hwin) v[i] -= s2;
+            if constexpr (EV & 1) v[i] -= s2;
+            if constexpr (EV & 2) {
               if (i == isuf) sufb = s2;
             }
             ring[i] = __builtin_fma(-2.0, xd, sh2);   // -2 (xd - sh), one rounding: exact scaling
           }
         }
       };
-      const bool plain = rem >= TW && !hwin && (isuf < 0 || isuf >= TW);
-      if (g == 0) {
-        if (plain) rows(std::true_type{}, std::true_type{}, std::true_type{});   // g = 0: dly always
-        else rows(std::false_type{}, std::true_type{}, std::true_type{});
-      } else {
-        // dly as a template argument: g is not wave-uniform to the compiler, so a runtime dly made
-        // every delayed read an exec-masked branch (a default move and mask saves per row)
-        if (dly) {
-          if (plain) rows(std::true_type{}, std::false_type{}, std::true_type{});
-          else rows(std::false_type{}, std::false_type{}, std::true_type{});
+      const bool suf = isuf >= 0 && isuf < TW;
+      const bool plain = rem >= TW && !hwin && !suf;
+      // dly and the chunk's events as template arguments: g is not wave-uniform to the compiler,
+      // so runtime flags made every delayed read an exec-masked branch (a default move and mask
+      // saves per row) and every row of an event chunk two selects
+      auto go = [&](auto mom_c, auto dly_c) {
+        if (plain) {
+          rows(std::true_type{}, mom_c, dly_c, std::integral_constant<int, 0>{});
         } else {
-          if (plain) rows(std::true_type{}, std::false_type{}, std::false_type{});
-          else rows(std::false_type{}, std::false_type{}, std::false_type{});
+          auto f = [&](auto ev_c) { rows(std::false_type{}, mom_c, dly_c, ev_c); };
+          static_dispatch<4>((hwin ? 1 : 0) | (suf ? 2 : 0), f);
         }
-      }
+      };
+      if (g == 0) go(std::true_type{}, std::true_type{});   // g = 0: dly always
+      else if (dly) go(std::false_type{}, std::true_type{});
+      else go(std::false_type{}, std::false_type{});
       if (cc == nch - 1) {                        // the split chain is complete
         // q4 = 4 (S2 - S2 through n-1-gofs) + sum of the ring's (-2 y)^2: 4x the T_t suffix sums,
         // exactly (power-of-2 scalings commute with rounding)
