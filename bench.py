@@ -468,7 +468,7 @@ def main():
                    n_eff_median=float(np.median(neff)), n_eff_min=float(np.min(neff)),
                    rhat_median=float(np.median(R_hat)), rhat_max=float(np.max(R_hat)),
                    samples_per_chain=n_samples, sampling_s=t_samples, diagnostics_s=diag_s,
-                   diagnostics_lags=None if sd is not None else dict(LAST_INFO),
+                   diagnostics_lags=dict(LAST_INFO),
                    method=(f"streaming statistics (tmax={a.tmax}) over every timed sample, fed inside the timed loop"
                            if sd is not None else
                            f"reference estimator on the circular window's last {R} samples per chain (all chains), "

@@ -76,6 +76,28 @@ def test_convergence_sums_vs_numpy(N, Niter, Dtot, d0, thin, wu, tmax):
     np.testing.assert_allclose(got, want, rtol=1e-10, atol=1e-9 * np.abs(want).max())
 
 
+@pytest.mark.parametrize("d0,d1,wu", [(3, 50, 0), (1, 101, 4), (0, 7, 2)])
+def test_convergence_stats_dim_sliced_view_vs_oracle(d0, d1, wu):
+    """convergence_stats on a non-contiguous, dim-sliced device view (q[:, 1:, d0:d1], row stride
+    != D): the shift S must be the view's own first sample, not a position in a flattened copy
+    (advisor r03).  R-hat and ESS equal the oracle's on the same NumPy slice."""
+    from hmc_amd import diagnostics as G
+    from oracle import hmc_oracle as O
+    rs = np.random.RandomState(11 + d0)
+    N, L, Dt = 16, 81, 101
+    x = np.empty((N, L, Dt))
+    x[:, 0] = rs.standard_normal((N, Dt))
+    for t in range(1, L):
+        x[:, t] = 0.6 * x[:, t - 1] + rs.standard_normal((N, Dt))
+    x += np.linspace(-30.0, 30.0, Dt)                  # per-dim offsets: a wrong shift shows
+    dev = torch.as_tensor(x).cuda()[:, 1:, d0:d1]
+    assert not dev.is_contiguous()
+    R, neff = G.convergence_stats(dev, thin_rate=1, warm_up_num=wu)
+    R_ref, neff_ref = O.convergence_stats(x[:, 1:, d0:d1], thin_rate=1, warm_up_num=wu)
+    np.testing.assert_allclose(R, R_ref, rtol=1e-10)
+    np.testing.assert_allclose(neff, neff_ref, rtol=1e-8)
+
+
 @pytest.mark.parametrize("D", [100, 7])
 def test_convergence_stats_n50_vs_oracle(D):
     """Split chains of n = 50 (the bench window): the one pass takes lags 1..48 (conv_tmax) and

@@ -83,6 +83,52 @@ def test_nuts_matches_oracle(case, fp_mode):
     np.testing.assert_allclose(h.dE_chain[:, :, 0], ref["dE_chain"], rtol=1e-8, atol=1e-9)
 
 
+@pytest.mark.parametrize("fp_mode", ["exact", "fast"])
+def test_nuts_deep_tree_single_chain_handoff(fp_mode):
+    """One chain, d_max = 14 and a step small enough for 2^12 .. 2^13-point trees (unit MVN, D = 2,
+    dt = 2e-3: 16,381 leapfrogs over 3 iterations), every iteration in ONE launch.  Iterations
+    2 and 3 are queued units of the same chain, so their slots wait thousands of wave steps for
+    the hand-off of the one before (samplers.py:595-598 with the deepest trees this d_max allows
+    short of the abort): no give-up may trip, and leapfrog counts and q_chain equal the oracle's."""
+    from hmc_amd.target import MVNTarget
+    D, N, Niter, d_max, dt = 2, 1, 3, 14, 2e-3
+    rs = np.random.RandomState(3)
+    q_start = rs.standard_normal((N, D))
+    p0 = rs.standard_normal((N, D))
+    P = rs.standard_normal((N, Niter, D))
+    tape = rs.uniform(0.0, 2.0, (N, Niter * 2 * (2 ** d_max + d_max + 2)))
+    core = O.HMCCore(O.MVNTarget(np.zeros(D), np.eye(D)), dt, None)
+    ref = O.gen_sample_nuts(core, q_start, N, Niter, 0, 1, d_max, O.ReplayDraws(p0, P, tape=tape.copy()),
+                            on_dmax="raise")
+    assert ref["n_leapfrog"] == 16381
+    h = _nuts(D, MVNTarget(np.zeros(D), np.eye(D)), N, Niter, 0, 1, dt, d_max, rng="replay", fp_mode=fp_mode)
+    h.set_nuts_replay(p0, P, tape)
+    h.gen_sample_NUTS(q_start, 0, False)              # raises on a give-up (CNT_HANDOFF_GIVEUP)
+    from hmc_amd import _lib as H
+    c = h.engine.read_counters()
+    assert c[H.CNT_HANDOFF_GIVEUP] == 0 and c[H.CNT_DMAX] == 0
+    assert h.n_leapfrog == ref["n_leapfrog"]
+    assert h.N_total_steps == ref["N_total_steps"]
+    np.testing.assert_allclose(h.q_chain, ref["q_chain"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(h.E_chain[:, :, 0], ref["E_chain"], rtol=1e-10, atol=1e-10)
+
+
+def test_nuts_replay_without_tape_warns():
+    """rng='replay' NUTS without set_nuts_replay cannot follow the reference's data-dependent
+    np.random order (samplers.py:608, :748, :773): it runs Philox seeded from np.random and says so."""
+    from hmc_amd.target import MVNTarget
+    D, N = 3, 4
+    h = _nuts(D, MVNTarget(np.zeros(D), np.eye(D)), N, 3, 0, 1, 0.2, 6, rng="replay")
+    np.random.seed(1)
+    with pytest.warns(UserWarning, match="Philox"):
+        h.gen_sample(np.zeros((N, D)), verbose=False)
+    np.random.seed(1)
+    h2 = _nuts(D, MVNTarget(np.zeros(D), np.eye(D)), N, 3, 0, 1, 0.2, 6, rng="replay")
+    with pytest.warns(UserWarning):
+        h2.gen_sample(np.zeros((N, D)), verbose=False)
+    assert np.array_equal(h.q_chain, h2.q_chain)     # np.random.seed still fixes the run
+
+
 def test_nuts_dmax_raises():
     from hmc_amd.target import MVNTarget
     D = 4

@@ -44,6 +44,54 @@ def test_windows_match_oracle(tmax, seg):
     np.testing.assert_allclose(neff[ok], neff_ref[ok], rtol=1e-10)
 
 
+@pytest.mark.parametrize("rho,tmax", [(0.97, 16), (0.6, 16), (0.9, 32)])
+def test_truncated_dims_count_matches_oracle_loop(rho, tmax):
+    """Slow-mixing chains: StreamingDiagnostics.finish() reports how many dimensions' reference
+    ESS loop (utils.py:139-152) reads a lag beyond tmax -- exactly the dims whose streamed n_eff is
+    a truncated sum -- and every other dim's n_eff equals the oracle's."""
+    from hmc_amd.diagnostics import LAST_INFO, StreamingDiagnostics
+    N, L = 24, 402
+    D = 40
+    rs = np.random.RandomState(int(rho * 100) + tmax)
+    rhos = np.linspace(0.0, rho, D)                              # mixing from fast to slow per dim
+    q = np.empty((N, L, D))
+    q[:, 0] = rs.standard_normal((N, D))
+    for t in range(1, L):
+        q[:, t] = rhos * q[:, t - 1] + np.sqrt(1 - rhos * rhos) * rs.standard_normal((N, D))
+    x = torch.as_tensor(q[:, 1:, :]).cuda()
+    sd = StreamingDiagnostics(N, D, L - 1, tmax=tmax)
+    p = 0
+    while p < L - 1:
+        rows = min(60, L - 1 - p)
+        carry = min(tmax, p)
+        sd.update(x[:, p - carry:p + rows, :], carry, rows)
+        p += rows
+    R, neff = sd.finish()
+    need = _lags_needed(q[:, 1:, :])
+    want = int((need > tmax).sum())
+    assert sd.info["truncated_dims"] == want and LAST_INFO["truncated_dims"] == want
+    if rho > 0.9:
+        assert want > 0                                         # the case this report exists for
+    _, neff_ref = O.convergence_stats(q[:, 1:, :], thin_rate=1, warm_up_num=0)
+    ok = need <= tmax
+    np.testing.assert_allclose(neff[ok], neff_ref[ok], rtol=1e-10)
+
+
+def test_sampler_streaming_warns_on_truncation():
+    """HMC_sampler(store_chain=False) with a tmax far below the chains' correlation time warns
+    that its streamed n_eff is truncated (and by how many dims)."""
+    from hmc_amd.samplers import HMC_sampler
+    D, N = 6, 16
+    tgt = O.MVNTarget(np.zeros(D), np.eye(D))
+    h = HMC_sampler(D, tgt.V, tgt.dVdq, Nchain=N, Niter=400, sampler_type="Random", L_low=1, L_high=2,
+                    dt=0.05, warm_up_num=0, store_chain=False, stream_tmax=8, iters_per_launch=20, rng="philox",
+                    seed=3)
+    h.gen_sample(np.full((N, D), 2.0), verbose=False)
+    with pytest.warns(UserWarning, match="truncated"):
+        h.compute_convergence_stats()
+    assert h.stream_info["truncated_dims"] > 0
+
+
 def _lags_needed(q):
     """Per dim, the largest variogram lag the reference's ESS loop reads (oracle restatement)."""
     chains, n = O.split_chains(q, thin_rate=1, warm_up_num=0)

@@ -71,10 +71,12 @@ __device__ __forceinline__ double ld_wt_d(const double* p) {
 // are handed out n apart, so at most ceil(slots / n) + 1 iterations of a chain are in flight and
 // each holder finishes within one tree, 2^(d_max+1) steps plus its transitions; a step of the
 // waiting wave costs about what a step of the holder's does (both run the MFMA gradient), and
-// the factor 4 covers the difference.
+// the factor 4 covers the difference.  A holder can still be slowed far more than that (clock or
+// XCD variation, several ranks sharing one GPU), so the cap never drops below 2^20 wave steps: a
+// give-up is a hard error and only a broken hand-off may trip it.
 inline unsigned nuts_wait_cap(int64_t slots, int64_t n, int d_max) {
   const int64_t inflight = (slots + n - 1) / std::max<int64_t>(n, 1) + 1;
-  const int64_t cap = 4 * inflight * ((int64_t(1) << (d_max + 1)) + 64);
+  const int64_t cap = std::max<int64_t>(4 * inflight * ((int64_t(1) << (d_max + 1)) + 64), int64_t(1) << 20);
   return (unsigned)std::min<int64_t>(cap, 0x7FFFFFFF);
 }
 
@@ -823,7 +825,7 @@ void k_nuts_iters(RandArgs a) {
     NUTS_PHASE(7);
   }
 #ifdef HMC_DEBUG_HOOKS
-  if (a.stamps && lane == 0) {
+  if (a.stamps && lane == 0 && wv < n_waves) {   // g_stamps has one row per workspace wave
 #pragma unroll
     for (int i = 0; i < 14; ++i) a.stamps[wv * kStampWords + i] = ph[i];
   }

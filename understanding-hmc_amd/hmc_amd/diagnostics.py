@@ -135,7 +135,9 @@ def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
     dev = sp.t.device
     tmax = conv_tmax(n)
     sums = convergence_sums(sp, tmax)
-    S = sp.t.reshape(-1)[sp.base:sp.base + D].to(torch.float64)          # the kernels' shift S_d
+    S = sp.t[0, warm_up_num, :].to(torch.float64)                       # the kernels' shift x[base + d]
+    # (a strided view of the stored sample: no copy of a non-contiguous q_chain view, and the
+    # right elements for dim-sliced views whose row stride is not D)
     m_loc = 2 * sp.Nchain
     # round 1: sum_j std_j, sum_j mean_j (= shifted sum + m S), variogram sums, split-chain count
     r1 = torch.cat([sums[0:1], (sums[1] + m_loc * S)[None], sums[3:],
@@ -160,7 +162,9 @@ def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
     T = v.shape[0]
     Vt = v / (m * (n - np.arange(1, T + 1)))[:, None]                   # utils.py:177
     n_eff, need = ess_vectorised(Vt, var_h, n, m, complete=T >= lmax)
-    LAST_INFO.update(tmax=tmax, lags=T, fallback_dims=int(need.sum()), fallback_passes=0)
+    LAST_INFO.clear()
+    LAST_INFO.update(mode="stored", tmax=tmax, lags=T, fallback_dims=int(need.sum()), fallback_passes=0,
+                     truncated_dims=0)
     if need.any():
         # the dims whose criterion reads lags > T: gather their columns once (one strided read of
         # the lines holding them) into a compact (N, 2n, k) copy, and run the lag blocks on it (the
@@ -310,12 +314,15 @@ def _colsum(x, center=None):
     return ((x - center) ** 2).sum(0) if center is not None else x.sum(0)
 
 
-def combine_split_stats(mean, std, vsum, n, group=None):
+def combine_split_stats(mean, std, vsum, n, group=None, info=None):
     """R-hat and ESS (utils.py:109-157) from this rank's split-chain moments mean/std
     (m_local, D), its variogram lag sums vsum (T, D) (vsum[t-1] = sum over its split chains of
     sum_s (x[s+t] - x[s])^2, lags 1..T) and the half length n.  Every quantity is a sum over
     split chains, so ranks all-reduce them (two rounds: B needs the global mean).  Lags stop
-    at T: the ESS sum ends there if the reference's criterion has not fired by then."""
+    at T: the ESS sum ends there if the reference's criterion has not fired by then.  `info`
+    (a dict) receives lags = T and truncated_dims = the number of dimensions whose reference
+    loop (utils.py:139-152) would have read a lag beyond T: their n_eff is the sum truncated at
+    T, not the reference's value."""
     dev = mean.device
     m = int(_allreduce(torch.tensor([float(mean.shape[0])], dtype=torch.float64, device=dev), group).item())
     assert m > 2                                                        # 2*Nchain, utils.py:85
@@ -333,7 +340,11 @@ def combine_split_stats(mean, std, vsum, n, group=None):
     lags = np.arange(1, T + 1)
     Vt = v / (m * (n - lags))[:, None]                                  # utils.py:177
     var_h = var.cpu().numpy()
-    n_eff, _ = ess_vectorised(Vt, var_h, n, m, complete=T >= n - 1, truncate=True)
+    complete = T >= n - 1
+    n_eff, _ = ess_vectorised(Vt, var_h, n, m, complete=complete, truncate=True)
+    if info is not None:
+        _, open_ = ess_vectorised(Vt, var_h, n, m, complete=complete, truncate=False)
+        info.update(lags=int(T), truncated_dims=int(open_.sum()), n_half=int(n))
     return R.cpu().numpy(), n_eff
 
 
@@ -378,6 +389,14 @@ class StreamingDiagnostics:
         return mean.reshape(2 * self.N, self.D), torch.sqrt(torch.clamp(var, min=0.0)).reshape(2 * self.N, self.D)
 
     def finish(self, group=None):
+        """(R, n_eff).  self.info (and diagnostics.LAST_INFO) then hold tmax, the lags used and
+        truncated_dims: how many dimensions' ESS criterion had not fired by lag tmax, i.e. whose
+        n_eff differs from the reference's (0 = every n_eff is the reference's)."""
         assert self.pos >= 2 * self.n, "not all split-chain samples were fed"
         mean, std = self.moments()
-        return combine_split_stats(mean, std, self.vsum, self.n, group)
+        info = dict(mode="streaming", tmax=self.tmax)
+        out = combine_split_stats(mean, std, self.vsum, self.n, group, info=info)
+        self.info = info
+        LAST_INFO.clear()
+        LAST_INFO.update(info)
+        return out

@@ -22,7 +22,7 @@ def _dev(a, device, dtype=torch.float64):
 class RandomEngine:
     def __init__(self, target, n_chains, n_iter, warm_up, thin, L_low, L_high, dt, cov_p=None, rng="philox",
                  seed=0, fp_mode="fast", chain_offset=0, store_chain=True, store_energy=True, n_save=0,
-                 device=None, dense=False, order_tiles=True):
+                 device=None, dense=False, order_tiles=True, random_ws=True):
         self.t = target
         self.D = D = target.D
         self.N = int(n_chains)
@@ -264,7 +264,8 @@ class NutsEngine(RandomEngine):
         # order_tiles=False: the NUTS kernel uses neither the tile order nor the gradient cache
         super().__init__(target, n_chains, n_iter, warm_up, thin, 5, 20, dt, cov_p=cov_p, rng=rng, seed=seed,
                          fp_mode=fp_mode, chain_offset=chain_offset, store_chain=store_chain,
-                         store_energy=store_energy, n_save=0, device=device, dense=True, order_tiles=False)
+                         store_energy=store_energy, n_save=0, device=device, dense=True, order_tiles=False,
+                         random_ws=False)
         assert on_dmax in ("raise", "break")
         self.d_max = int(d_max)
         self.on_dmax = 0 if on_dmax == "raise" else 1

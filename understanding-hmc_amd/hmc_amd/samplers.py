@@ -18,6 +18,7 @@ Randomness (new optional kwarg `rng`):
     equivalent, independent of launch geometry and GPU count.
 """
 import time
+import warnings
 
 import numpy as np
 import torch
@@ -273,6 +274,12 @@ class HMC_sampler(sampler):
         diag = getattr(self, "_stream_diag", None)
         if diag is not None:
             self.R_q, self.n_eff_q = diag.finish()
+            self.stream_info = dict(diag.info)
+            if diag.info["truncated_dims"]:
+                warnings.warn("streaming ESS: %d of %d dimensions need variogram lags beyond stream_tmax=%d; "
+                              "their n_eff is the sum truncated there, not the reference's value "
+                              "(raise stream_tmax or store q_chain)"
+                              % (diag.info["truncated_dims"], self.D, diag.tmax), UserWarning, stacklevel=2)
             return
         sampler.compute_convergence_stats(self)
 
@@ -326,6 +333,11 @@ class HMC_sampler(sampler):
         tape = getattr(self, "_nuts_replay", None)
         rng, seed = self.rng, self.seed
         if rng == "replay" and tape is None:
+            # the reference draws directions and uniforms from np.random in a data-dependent order
+            # (:608, :748, :773) that chain-parallel trees cannot follow: say that this run differs
+            warnings.warn("NUTS rng='replay' without set_nuts_replay(): running Philox streams seeded "
+                          "from np.random (reproducible, statistically equivalent, not the reference's "
+                          "draws)", UserWarning, stacklevel=2)
             rng, seed = "philox", int(np.random.randint(0, 2 ** 62, dtype=np.int64))
         eng = NutsEngine(self.target(), self.Nchain, self.Niter, self.warm_up_num, self.thin_rate, self.d_max,
                          self.dt, cov_p=self.cov_p, rng=rng, seed=seed, fp_mode=self.fp_mode,
