@@ -385,7 +385,7 @@ def main():
     tgt = MVNTarget(np.zeros(D), cov)
     if nuts:
         eng = NutsEngine(tgt, N, n_iter, wu, 1, a.d_max, a.dt, rng="philox", seed=a.seed, fp_mode=a.fp_mode,
-                         chain_offset=offset, store_chain=False, on_dmax="break", device=dev)
+                         chain_offset=offset, store_chain=False, on_dmax="break", device=dev, iters_per_call=S)
     else:
         eng = RandomEngine(tgt, N, n_iter, wu, 1, 5, 20, a.dt, rng="philox", seed=a.seed, fp_mode=a.fp_mode,
                            chain_offset=offset, store_chain=False, device=dev, order_tiles=not a.no_order_tiles)

@@ -170,8 +170,14 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
 /* Bytes of the optional hmc_state.order scratch for hmc_random_iters on this target
  * (0 for diagonal targets, which need none): the tile order plus the gradient cache. */
 int64_t hmc_random_workspace_size(const hmc_target* t, int64_t n_chains);
-/* Bytes of device workspace hmc_nuts_iters needs for n_chains chains (tree vectors: live
- * points, both boundaries, d_max+1 save slots; replay-tape cursors).  0 if unsupported. */
+/* Bytes of device workspace hmc_nuts_iters needs for n_chains chains: tree vectors (live points,
+ * both boundaries, d_max+1 save slots), replay-tape cursors, the launch's work queue and, for
+ * Philox runs with a diagonal cov_p (philox_momenta != 0), the momenta drawn ahead of the tree
+ * kernel: n_chains x min(32, iters_per_call) x 16*ceil(D/16) doubles (iters_per_call = the largest
+ * iter_end - iter_begin the caller will pass).  0 if unsupported.
+ * hmc_nuts_workspace_size(D, n, d_max) = ..._ex(D, n, d_max, 32, 1): enough for any call. */
+int64_t hmc_nuts_workspace_size_ex(int32_t D, int64_t n_chains, int32_t d_max, int32_t iters_per_call,
+                                   int32_t philox_momenta);
 int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max);
 
 /* Iterations [iter_begin, iter_end) of the No-U-Turn sampler for all chains: momentum

@@ -305,10 +305,15 @@ int64_t hmc_random_workspace_size(const hmc_target* t, int64_t n_chains) {
   return hmc::dense_workspace_bytes(n_chains, t->D);
 }
 
-int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max) {
-  if (D < 1 || n_chains < 0 || d_max < 1 || d_max > 15) return 0;
+int64_t hmc_nuts_workspace_size_ex(int32_t D, int64_t n_chains, int32_t d_max, int32_t iters_per_call,
+                                   int32_t philox_momenta) {
+  if (D < 1 || n_chains < 0 || d_max < 1 || d_max > 15 || iters_per_call < 1) return 0;
   if (!hmc::dense_tiles(D)) return hmc::nuts_big_ws_doubles(n_chains, D, d_max) * (int64_t)sizeof(double);
-  return hmc::nuts_ws_doubles(n_chains, D, d_max) * (int64_t)sizeof(double);
+  return hmc::nuts_ws_doubles(n_chains, D, d_max, philox_momenta ? iters_per_call : 0) * (int64_t)sizeof(double);
+}
+
+int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max) {
+  return hmc_nuts_workspace_size_ex(D, n_chains, d_max, 32, 1);
 }
 
 hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, const hmc_replay* r,
@@ -431,14 +436,14 @@ hmc_status hmc_rowsum(const double* x, int64_t n_outer, int64_t outer_stride, in
 hmc_status hmc_variogram(const double* x, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
                          int64_t base, int32_t n, int32_t D, int32_t t0, int32_t t1, double* work, double* out,
                          void* stream) {
-  if (!x || !work || !out || n_chains < 1 || n < 1 || D < 1 || t0 < 1 || t1 <= t0)
+  if (!x || !work || !out || n_chains < 1 || n < 1 || D < 1 || t0 < 1 || t1 <= t0 || t1 - t0 > 4096)
     return fail(HMC_EINVAL, "bad arguments");
   return hip_status(hmc::launch_variogram(x, n_chains, chain_stride, sample_stride, base, n, D, t0, t1, work, out,
                                           (hipStream_t)stream),
                     "hmc_variogram");
 }
 
-static bool conv_tmax_ok(int32_t t) { return t == 8 || t == 16 || t == 32 || t == 48 || t == 64; }
+static bool conv_tmax_ok(int32_t t) { return t >= 1 && t <= 4096; }
 
 int64_t hmc_convergence_work_size(int64_t n_chains, int32_t D, int32_t tmax) {
   if (n_chains < 1 || D < 1 || !conv_tmax_ok(tmax)) return 0;
@@ -449,7 +454,7 @@ hmc_status hmc_convergence_sums(const double* x, int64_t n_chains, int64_t chain
                                 int64_t base, int32_t n, int32_t D, int32_t tmax, double* work, double* out,
                                 void* stream) {
   if (!x || !work || !out || n_chains < 1 || n < 2 || D < 1) return fail(HMC_EINVAL, "bad arguments");
-  if (!conv_tmax_ok(tmax)) return fail(HMC_EINVAL, "tmax must be 8, 16, 32, 48 or 64");
+  if (!conv_tmax_ok(tmax)) return fail(HMC_EINVAL, "tmax must be in 1 .. 4096");
   return hip_status(hmc::launch_conv_fused(x, n_chains, chain_stride, sample_stride, base, n, D, tmax, work, out,
                                            (hipStream_t)stream),
                     "hmc_convergence_sums");

@@ -110,194 +110,16 @@ __global__ __launch_bounds__(256) void k_colsum_acc(const double* partial, int64
   out[c] += acc;
 }
 
-// partial[chunk][k][d] = sum over the chunk's split chains j of sum_s (x_j[s+t]-x_j[s])^2 for the lags
-// t = t0 + k, k < nt <= T.  ONE pass over the samples (round 1 re-read the chain once per lag):
-// each thread walks its chains' samples s = t0 .. n-1 with a register ring holding
-// x[s-t0], x[s-t0-1], ..., x[s-t0-T+1]; per sample it reads x[s] and the delayed x[s-t0] (the same
-// value for t0 = 1, a second, cache-friendly stream otherwise).  Lane = dim: coalesced rows.
-template <int T>
-__global__ __launch_bounds__(256) void k_variogram_ring(Src s, int t0, int nt, int64_t jchunk, double* partial) {
-  __shared__ double red[4][kDimTile];
-  const int dl = threadIdx.x & (kDimTile - 1);
-  const int rl = threadIdx.x / kDimTile;
-  const int d = blockIdx.y * kDimTile + dl;
-  const int64_t j0 = (int64_t)blockIdx.x * jchunk;
-  const int64_t j1 = min(j0 + jchunk, 2 * s.n_chains);
-  const int64_t ss = s.sample_stride;
-  double v[T];
-#pragma unroll
-  for (int k = 0; k < T; ++k) v[k] = 0.0;
-  if (d < s.D) {
-    for (int64_t j = j0 + rl; j < j1; j += 4) {
-      const double* b = split_ptr(s, j, 0) + d;
-      double ring[T];
-#pragma unroll
-      for (int k = 0; k < T; ++k) ring[k] = 0.0;
-      int i = t0;
-      // fill: ring slot k is valid once i - t0 >= k
-      for (; i < s.n && i - t0 < T - 1; ++i) {
-#pragma unroll
-        for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
-        ring[0] = b[(int64_t)(i - t0) * ss];
-        const double x = b[(int64_t)i * ss];
-#pragma unroll
-        for (int k = 0; k < T; ++k) {
-          const double e = x - ring[k];
-          v[k] = (k <= i - t0) ? __builtin_fma(e, e, v[k]) : v[k];
-        }
-      }
-      for (; i < s.n; ++i) {
-#pragma unroll
-        for (int k = T - 1; k > 0; --k) ring[k] = ring[k - 1];
-        ring[0] = b[(int64_t)(i - t0) * ss];
-        const double x = b[(int64_t)i * ss];
-#pragma unroll
-        for (int k = 0; k < T; ++k) {
-          const double e = x - ring[k];
-          v[k] = __builtin_fma(e, e, v[k]);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < T; ++k) {
-    if (k < nt) {
-      red[rl][dl] = v[k];
-      __syncthreads();
-      if (rl == 0 && d < s.D)
-        partial[((int64_t)blockIdx.x * nt + k) * s.D + d] = ((red[0][dl] + red[1][dl]) + red[2][dl]) + red[3][dl];
-      __syncthreads();
-    }
-  }
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ int64_t uni(int64_t x) {
+  return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)((uint64_t)x >> 32)) << 32) |
+                   (uint32_t)__builtin_amdgcn_readfirstlane((int)x));
+}
+template <class T>
+__device__ __forceinline__ T* uni(T* p) {
+  return reinterpret_cast<T*>(uni((int64_t)(uintptr_t)p));
 }
 
-// ---- ONE pass for convergence_stats (utils.py:88-126 and :161-179).  Per split chain j (n samples)
-// and dim d, with y = x - x_j[0] (shifted: the sums stay well conditioned):
-//   mean_j = (x[0] + x[1] + ... + x[n-1]) / n, summed in sample order without FMA: NumPy's np.mean
-//   over axis 0 bit for bit (np.std(ddof=1) at utils.py:109-112 starts from it);
-//   s1 = sum y, S2 = sum y^2, delta = mean_j - x_j[0]:
-//   sum (x - mean_j)^2 = S2 - 2 delta s1 + n delta^2 (NumPy's second pass, up to rounding: for a chain
-//   that never moved, e.g. every proposal rejected, it is n delta^2 with NumPy's own delta, so
-//   W = mean std_j keeps the reference's rounding-level value instead of an exact 0)
-//   V_t,j = sum_{s<n-t} (y[s+t] - y[s])^2 = 2 S2 - H_t - T_t - 2 C_t,  C_t = sum_s y[s] y[s-t],
-//   H_t = sum_{s<t} y^2 (the first t samples), T_t = sum_{s>=n-t} y^2 (the last t)
-// so a lag costs ONE FMA per sample (v += (-2 y[s]) y[s-t] against a register ring) instead of a
-// subtraction and an FMA.  The lags are split over G waves (lag group g: lags gTW+1 .. gTW+TW, a
-// ring fed by the sample stream delayed by gTW), so T = G*TW lags fit the register file:
-//   * samples run in chunks of TW; chunk g is exactly the positions whose running S2 is H_t of
-//     this wave's lags (static register index inside the unrolled chunk);
-//   * at the end the ring holds y[n-1-gTW-k], so T_t = (S2 - S2 through position n-1-gTW) +
-//     cumulative squares of the ring.
-// Sums over the block's split chains:
-//   row 0: sum_j std_j, row 1: sum_j (mean_j - S_d), row 2: sum_j (mean_j - S_d)^2,
-//   row 3 + t - 1: sum_j V_t,j for lags t = 1..T (valid for t < n), S_d = x[base + d].
-// Block = 4 waves = 4/G split chains at a time x G lag groups, lane = dim (coalesced rows).  The dim
-// tiles of one chain group run on the same XCD (block b on XCD b % 8), so a row's line shared by
-// two tiles is fetched from HBM once.
-template <int TW, int G>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_conv_lags(Src s, int groups,
-                                                                                             int ntiles,
-                                                                                             double* partial) {
-  constexpr int SL = 4 / G;             // split chains per block at a time
-  constexpr int T = TW * G;
-  __shared__ double red[4][kDimTile];
-  const int dl = threadIdx.x & (kDimTile - 1);
-  const int w = threadIdx.x / kDimTile;
-  const int slot = w / G, g = w % G;    // wave-uniform
-  const int gofs = g * TW;              // this wave's lags: gofs + 1 .. gofs + TW
-  const int b = blockIdx.x;             // XCD-aware: tiles of a group 8 blocks apart
-  const int tile = (b >> 3) % ntiles;
-  const int grp = (b & 7) + 8 * ((b >> 3) / ntiles);
-  const int d = tile * kDimTile + dl;
-  const int64_t m2 = 2 * s.n_chains;
-  const int64_t ss = s.sample_stride;
-  const int n = s.n;
-  double v[TW];
-#pragma unroll
-  for (int k = 0; k < TW; ++k) v[k] = 0.0;
-  double a_std = 0.0, a_m = 0.0, a_m2 = 0.0, a_last = 0.0;
-  if (d < s.D && grp < groups && slot < SL) {   // (G = 3: the fourth wave idles)
-    const double S = s.x[s.base + d];
-    const int pos_suf = n - gofs - 1;   // T_t needs S2 through this position
-    for (int64_t j = (int64_t)grp * SL + slot; j < m2; j += (int64_t)groups * SL) {
-      const double* bp = split_ptr(s, j, 0) + d;
-      const double sh = bp[0];
-      double ring[TW];
-#pragma unroll
-      for (int k = 0; k < TW; ++k) ring[k] = 0.0;
-      double s1 = 0.0, s2 = 0.0, r1 = 0.0, sufb = 0.0;
-      for (int c0 = 0; c0 < n; c0 += TW) {
-        double xc[TW], xd[TW];
-#pragma unroll
-        for (int i = 0; i < TW; ++i) {
-          const int sp = c0 + i, sq = sp - gofs;
-          xc[i] = sp < n ? bp[(int64_t)sp * ss] : 0.0;
-          xd[i] = (sq >= 0 && sq < n) ? bp[(int64_t)sq * ss] : sh;   // delayed stream (y = 0 before 0)
-        }
-        const bool hwin = c0 == gofs;   // uniform: this chunk's running S2 gives H_t of our lags
-#pragma unroll
-        for (int i = 0; i < TW; ++i) {
-          const int sp = c0 + i;
-          if (sp < n) {                 // uniform
-            r1 += xc[i];
-            const double y = xc[i] - sh;
-            s1 += y;
-            s2 = __builtin_fma(y, y, s2);
-            const double ym2 = -2.0 * y;
-#pragma unroll
-            for (int k = 0; k < TW; ++k) v[k] = __builtin_fma(ym2, ring[k], v[k]);
-            if (hwin) v[i] -= s2;       // H_t, t = gofs + 1 + i
-            if (sp == pos_suf) sufb = s2;
-#pragma unroll
-            for (int k = TW - 1; k > 0; --k) ring[k] = ring[k - 1];
-            ring[0] = xd[i] - sh;       // y[sp - gofs]
-          }
-        }
-      }
-      // ring[k] = y[n-1-gofs-k]: T_t = (S2 - S2 through n-1-gofs) + sum_{k' <= k} ring[k']^2
-      double q = pos_suf >= 0 ? s2 - sufb : s2;
-      const double s2x2 = 2.0 * s2;
-#pragma unroll
-      for (int k = 0; k < TW; ++k) {
-        q = __builtin_fma(ring[k], ring[k], q);
-        v[k] += s2x2 - q;
-      }
-      const double mean = r1 / n;
-      const double dm = mean - sh;
-      const double mm2 = (s2 - 2.0 * dm * s1) + n * (dm * dm);
-      a_std += sqrt(mm2 > 0.0 ? mm2 / (n - 1) : 0.0);
-      const double e = mean - S;
-      a_m += e;
-      a_m2 = __builtin_fma(e, e, a_m2);
-      const double yl = bp[(int64_t)(n - 1) * ss] - sh;   // lag n - 1: (x[n-1] - x[0])^2
-      a_last = __builtin_fma(yl, yl, a_last);
-    }
-  }
-  auto put = [&](int row, double x) {
-    red[w][dl] = x;
-    __syncthreads();
-    if (w == 0 && d < s.D && grp < groups)
-      partial[((int64_t)grp * (T + 4) + row) * s.D + d] = ((red[0][dl] + red[1][dl]) + red[2][dl]) + red[3][dl];
-    __syncthreads();
-  };
-  put(0, g == 0 ? a_std : 0.0);
-  put(1, g == 0 ? a_m : 0.0);
-  put(2, g == 0 ? a_m2 : 0.0);
-#pragma unroll
-  for (int gg = 0; gg < G; ++gg) {
-#pragma unroll
-    for (int k = 0; k < TW; ++k) put(3 + gg * TW + k, g == gg && gg * TW + k + 1 < s.n ? v[k] : 0.0);   // lags t >= n: 0
-  }
-  put(3 + T, g == 0 && s.n >= 2 ? a_last : 0.0);  // lag n - 1 (the ESS loop's last), whatever T
-}
-
-// The same sums with the series staged through LDS: each block runs SL = 4/G split chains at a time
-// (G waves each, one per lag group, as k_conv_lags) through a per-slot LDS ring of rows (lane = dim).
-// The G waves of a slot bring the slot's next rows in with direct-to-LDS loads
-// (global_load_lds_dwordx4: 16 B per lane, two 512-B rows per wave-instruction, no registers),
-// PD chunks of TW rows ahead, and every wave reads its current row and its delayed row (gTW back)
-// from the ring: one HBM read per element, no load buffers in registers, and the loads of PD
-// chunks in flight behind the lag products (the register-staged k_conv_lags is latency-bound).
 // f(std::integral_constant<int, r>) for the runtime r in [0, N): a uniform branch to one of N
 // statically indexed bodies
 template <class F, int... I>
@@ -308,127 +130,225 @@ template <int N, class F>
 __device__ __forceinline__ void static_dispatch(int r, F& f) {
   static_dispatch_(r, f, std::make_integer_sequence<int, N>{});
 }
-
-// this lane's id in its wave, recomputed where it is used (volatile: never kept live across a
-// loop, which costs two VALU instead of a register or a scratch reload)
-__device__ __forceinline__ int lane_id() {
-  int l;
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-  return l;
+// f(std::integral_constant<int, i>) for i = 0 .. N-1 in order: a source-level unroll (bodies too
+// large for the loop unroller's pragma threshold)
+template <class F, int... I>
+__device__ __forceinline__ void static_for_(F& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F& f) {
+  static_for_(f, std::make_integer_sequence<int, N>{});
 }
 
-// waves per block, and waves per SIMD (the launch bound: registers) of k_conv_lds<TW, G, 2>; the
-// LDS ring allows 4 / 3 / 2 / 1 / 3 blocks per CU for G = 3 / 4 / 2 / 1 (TW 16) / 1 (TW 8)
-constexpr int conv_waves(int G) { return G == 3 ? 3 : 4; }
-constexpr int conv_wpe(int TW, int G) { return G >= 3 ? 3 : G == 2 ? 2 : TW == 16 ? 1 : 3; }
+// ---- The variogram lag sums and split-chain moments of convergence_stats (utils.py:88-126,
+// :161-179) in ONE read of the samples, for any lag range.
+//
+// A *series* is one dimension d of one split chain j (n samples), flattened e = j*D + d; a wave
+// owns 64 consecutive series (a tile: every lane busy whatever D; rows of a split chain are
+// contiguous, so a wave's row load is one or two coalesced segments) and walks their n samples
+// once.  Per series, with y = x - x_j[0] (shifted: well-conditioned sums),
+//   V_t = sum_{s=t}^{n-1} (y_s - y_{s-t})^2 = 2 S2 - P(t) - Q(t) - 2 C_t,
+//   C_t = sum_s y_s y_{s-t},  P(t) = sum_{s<t} y_s^2,  Q(t) = sum_{s>=n-t} y_s^2,
+// so a lag costs ONE FMA per sample against a register ring of TL delayed samples.  A wave takes
+// the TL lags t = gofs + 1 .. gofs + TL (lag group g: gofs = L0 + g*TL); its ring is fed by the
+// sample stream delayed by gofs (the stream itself for gofs = 0).  Rows run in unrolled chunks of
+// TL from row gofs, so ring slots are static registers:
+//   * chunk 0 is the ramp: lag k of row i only meets the slots already written (k < i), so the
+//     products with samples before the series start are never issued -- the pass costs the
+//     triangle sum_t (n - t) of the reference's loop, not n*T -- and row i's running S2 is P(t);
+//   * the delayed stream's squares over the run are P(n - gofs), from which Q(t) follows with the
+//     ring's final contents (the last TL delayed samples);
+//   * rows 0 .. gofs - 1 (lag groups with gofs > 0) only add their squares to S2.
+// Lag group 0 of a first pass (L0 = 0) also sums the moments (mean_j: the samples added in order
+// without FMA, NumPy's np.mean over axis 0 bit for bit; std_j (ddof 1) from S2 and s1) and the
+// lag n - 1 the ESS loop reads last.
+// Determinism: a wave owns the tiles tau = c + C (r + R i) of one class c (C = D / gcd(D, 64): lane
+// l of every such tile holds dimension (64 c + l) mod D) and sums them in order in its lanes;
+// k_lag_classes / k_lag_dims add the waves' lanes per dimension in a fixed order.  Wave ids are
+// XCD-major (blocks b, b + 8, ... share an XCD): the lag groups of one (class, replica) run on the
+// same XCD, so the rows one group reads are L2 hits for the others.
+#ifndef HMC_LAG_TL
+#define HMC_LAG_TL 48
+#endif
+#ifndef HMC_LAG_PF
+#define HMC_LAG_PF 16
+#endif
+#ifndef HMC_LAG_WPE
+#define HMC_LAG_WPE 1
+#endif
+// Lags per wave, rows in flight per stream and waves per SIMD.  One wave per SIMD with the whole
+// register file, 48 lags (n = 50, the bench window, needs lags 1..48 + n - 1: one wave per tile) and
+// 16 rows in flight measured best on the bench window (29 ms; 32 lags at two waves per SIMD: 65 ms,
+// 53 ms with the ragged rows masked instead of branched; 48 lags at two waves per SIMD spill).
+constexpr int kLagTL = HMC_LAG_TL;
+constexpr int kLagPF = HMC_LAG_PF;   // divides kLagTL
+constexpr int kLagRows = kLagTL + 4;   // partial rows per wave: std, mean - S, (mean - S)^2, lag n-1, lags
+constexpr int kLagWaves = 8192;        // target waves per pass (4 rounds of 2 waves per SIMD)
+constexpr int kLagOOB = 0x40000000;    // buffer bound: lanes past the last series read zeros
 
-template <int TW, int G, int PD>
-__global__ __launch_bounds__(64 * conv_waves(G), conv_wpe(TW, G)) void k_conv_lds(Src s, int groups, int ntiles,
-                                                                                  double* partial) {
-  constexpr int NW = conv_waves(G);               // waves per block
-  constexpr int SL = NW / G;                      // split chains per block at a time
-  constexpr int T = TW * G;
-  constexpr int RB = (G + PD) * TW;               // ring rows per slot (multiple of TW)
-  constexpr int NP = TW / 2;                      // DMA instructions per chunk (2 rows each)
-  static_assert(SL * G == NW && TW % 2 == 0 && (TW & (TW - 1)) == 0, "layout");
-  __shared__ double ring_x[SL * RB * kDimTile];   // (the final reduction reuses it)
-  const int lane = threadIdx.x & (kDimTile - 1);
-  const int dl = lane;
-  const int w = threadIdx.x / kDimTile;
-  const int slot = w / G, g = w % G;
-  const int gofs = g * TW;
-  const int b = blockIdx.x;                       // XCD-aware: tiles of a group 8 blocks apart
-  const int tile = (b >> 3) % ntiles;
-  const int grp = (b & 7) + 8 * ((b >> 3) / ntiles);
-  const int d = tile * kDimTile + dl;
+struct LagArgs {
+  Src s;
+  int L0;          // lags L0 + 1 .. L0 + T (L0 a multiple of kLagPF)
+  int T;           // lags of this pass
+  int G;           // lag groups, ceil(T / TL)
+  int C, R;        // classes, replicas per class
+  int mom;         // group 0 sums the moments and lag n - 1 (first pass)
+  int64_t NT;      // tiles of 64 series
+  int rowb;        // bytes between samples (sample_stride * 8)
+};
+
+__host__ __device__ inline int lag_gcd(int a, int b) {
+  while (b) {
+    const int t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
+// The tiles of one wave.  Z: the lag group starts at lag 1 (gofs = 0: the ring is fed by the
+// stream itself; also the moments), else gofs > 0 (a second, delayed stream).  The two forms are
+// separate non-inlined functions so that each gets its own register allocation (one kernel
+// holding both spilled at 256 registers).
+template <int TL, int PF, bool Z>
+__device__ __forceinline__ void lag_wave(const LagArgs& a_, int W_, int g_, int c_, int r_, double* partial_) {
+  // a function's arguments arrive in VGPRs: make every launch constant uniform again (SGPRs), so
+  // that row and chunk tests stay scalar branches
+  LagArgs a;
+  a.s.x = uni(a_.s.x);
+  a.s.chain_stride = uni(a_.s.chain_stride);
+  a.s.sample_stride = uni(a_.s.sample_stride);
+  a.s.base = uni(a_.s.base);
+  a.s.n_chains = uni(a_.s.n_chains);
+  a.s.n = uni(a_.s.n);
+  a.s.D = uni(a_.s.D);
+  a.L0 = uni(a_.L0);
+  a.T = uni(a_.T);
+  a.G = uni(a_.G);
+  a.C = uni(a_.C);
+  a.R = uni(a_.R);
+  a.mom = uni(a_.mom);
+  a.NT = uni(a_.NT);
+  a.rowb = uni(a_.rowb);
+  const int W = uni(W_), g = uni(g_), c = uni(c_), r = uni(r_);
+  double* const partial = uni(partial_);
+  const int lane = threadIdx.x;
+  const Src& s = a.s;
+  const int n = s.n, D = s.D;
+  const int gofs = a.L0 + g * TL;
+  const bool mom = Z && a.mom;                     // wave-uniform (Z: gofs == 0, group 0)
   const int64_t m2 = 2 * s.n_chains;
-  const int n = s.n;
-  const int nch = (n + TW - 1) / TW;              // chunks per split chain
-  const int64_t stride = (int64_t)groups * SL;
-  const int64_t j0 = (int64_t)grp * SL;
-  const int K = grp < groups ? (int)((m2 - j0 + stride - 1) / stride) : 0;   // split chains per slot (max)
-  const int F = K * nch;                          // (split chain, chunk) items, the same for all slots
-  double* const my = ring_x + slot * RB * kDimTile;
-  // DMA of item f into ring rows (f TW) % RB ...: wave g moves row pairs g, g + G, ... of the chunk
-  constexpr int NI = (NP + G - 1) / G;            // DMA instructions per wave and chunk (G = 3: the
-                                                  // last wave repeats pair NP - 1: same bytes, same place)
-  const int dcol = (lane & 31) * 2;               // this lane's dim pair (and row lane >> 5 of 2)
-  // per-lane part of a DMA address: this lane's dim pair (pair 0 for the dims past D: loaded,
-  // never read), and rows clamped into the split chain (rows past n are loaded, never read)
-  const int dofs = tile * kDimTile + dcol < s.D ? tile * kDimTile + dcol : 0;
-  auto issue = [&](int f) {
-    const int64_t j = j0 + slot + (int64_t)(f / nch) * stride;
-    const int cc = f % nch;
-    const double* rb = split_ptr(s, j < m2 ? j : m2 - 1, 0);   // wave-uniform
-    rb = reinterpret_cast<const double*>(
-        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)rb >> 32)) << 32) |
-        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)rb));
-    const int r0 = (f * TW) % RB;
+  // lane -> (split chain jj past the tile's first, dim d): the same for every tile of the class
+  const int per = 64 / lag_gcd(D, 64);             // split chains per class period (64 C / D)
+  const int d0 = (int)((64 * (int64_t)c) % D);
+  const int jj = (d0 + lane) / D;
+  const int d = d0 + lane - jj * D;
+  int64_t j0 = (64 * (int64_t)c) / D + (int64_t)per * r;
+  const int64_t jstep = (int64_t)per * a.R;
+
+  double v[TL];
 #pragma unroll
-    for (int e = 0; e < NI; ++e) {
-      const int rr = 2 * min(g + G * e, NP - 1);  // row pair inside the chunk
-      const int row = min(cc * TW + rr + (lane_id() >> 5), n - 1);
-      const double* src = rb + (int64_t)row * s.sample_stride + dofs;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(my + (r0 + rr) * kDimTile),
-                                       16, 0, 0);
-    }
-  };
-  double v[TW];
-#pragma unroll
-  for (int k = 0; k < TW; ++k) v[k] = 0.0;
+  for (int k = 0; k < TL; ++k) v[k] = 0.0;
   double a_std = 0.0, a_m = 0.0, a_m2 = 0.0, a_last = 0.0;
-  const double S = d < s.D ? s.x[s.base + d] : 0.0;
-  asm volatile("" ::"v"(S));                      // landed before the ring's loads are in flight: a
-                                                  // later first use would wait for vmcnt(0)
-  // ring slot i holds -2 (x_delayed - shift) of chunk row i (the chunks are TW-aligned), so at row
-  // i lag gofs + 1 + k reads slot (i - 1 - k) mod TW: static registers, no ring shifts, and the
-  // lag product is one FMA (-2 y x_d: scaling by -2 is exact)
-  double ring[TW];
-  double sh = 0.0, sh2 = 0.0, s1 = 0.0, s2 = 0.0, r1 = 0.0, sufb = 0.0;
-  const int pos_suf = n - gofs - 1;
-  for (int f = 0; f < PD && f < F; ++f) issue(f);
-  for (int f = 0; f < F; ++f) {
-    // item f's rows have landed (PD - 1 newer items may still fly), and every wave is past item f-1
-    if (f + PD - 1 < F) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((PD - 1) * NI) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (f + PD < F) issue(f + PD);
-    const int64_t j = j0 + slot + (int64_t)(f / nch) * stride;
-    const int cc = f % nch;
-    const int rc = (f * TW) % RB;                 // ring row of this chunk's first row
-    const int rd = (rc - gofs + RB) % RB;         // ... of the delayed stream's
-    if (j < m2 && d < s.D) {
-      if (cc == 0) {                              // a split chain starts
-        sh = my[rc * kDimTile + lane_id()];
-        sh2 = 2.0 * sh;
+  const double Sd = s.x[s.base + d];               // shift of rows 1-2: the view's first sample
+  if (gofs + 1 < n || mom) {
+    // a tile's buffer descriptor and lane offset: split chain j0's first sample (wave-uniform) is the
+    // base; lane offsets in bytes (host-checked below kLagOOB); lanes past the last series read
+    // zeros (out of the buffer's range)
+    auto tile_rsrc = [&](int64_t jt, int& vo) {
+      const int64_t j = jt + jj;
+      const double* tb = split_ptr(s, jt, 0);
+      tb = reinterpret_cast<const double*>(
+          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)tb >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)tb));
+      vo = j < m2 ? (int)((split_ptr(s, j, 0) + d - tb) * 8) : kLagOOB + 64;
+      return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(tb), 0, kLagOOB, 0x00020000);
+    };
+    // the first PF rows of the NEXT tile are loaded a whole tile ahead (a tile's first rows used to
+    // wait a full memory latency: one wave per SIMD has nothing else to run meanwhile)
+    double xn[PF];
+    int voff_n = 0;
+    __amdgpu_buffer_rsrc_t rs_n = tile_rsrc(j0, voff_n);
+    const int64_t tau0 = c + (int64_t)a.C * r;
+    if (tau0 < a.NT) {
 #pragma unroll
-        for (int k = 0; k < TW; ++k) ring[k] = 0.0;
-        s1 = s2 = r1 = sufb = 0.0;
+      for (int p = 0; p < PF; ++p)
+        xn[p] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs_n, voff_n, (p < n ? p : n - 1) * a.rowb, 0));
+    }
+    for (int64_t tau = tau0; tau < a.NT; tau += (int64_t)a.C * a.R, j0 += jstep) {
+      const bool valid = j0 + jj < m2;
+      const __amdgpu_buffer_rsrc_t rs = rs_n;
+      const int voff = voff_n;
+      double xq[PF], xdq[PF];
+#pragma unroll
+      for (int p = 0; p < PF; ++p) {
+        xq[p] = xn[p];
+        if constexpr (!Z) xdq[p] = xn[p];            // loop B's delayed rows 0 .. PF-1 (PF <= gofs)
       }
-      const int rem = n - cc * TW;                // rows of this chunk
-      const bool hwin = cc * TW == gofs;          // this chunk's running S2 gives H_t of our lags
-      const bool dly = cc * TW >= gofs;           // the delayed rows exist (gofs is a multiple of TW)
-      const int isuf = pos_suf - cc * TW;         // suffix mark (T_t terms), if inside this chunk
-      auto rows = [&](auto plain_c, auto mom_c, auto dly_c, auto ev_c) {
-        constexpr bool PLAIN = decltype(plain_c)::value;   // whole chunk, no H_t / suffix event
-        constexpr bool MOM = decltype(mom_c)::value;       // lag group 0 also sums the moments
-        constexpr bool DLY = decltype(dly_c)::value;       // the delayed rows exist (else: the shift)
-        constexpr int EV = decltype(ev_c)::value;          // events in this chunk: 1 H_t, 2 suffix mark
-        // rows one ahead: row i + 1's two LDS reads are issued before row i's FMAs, and no later
-        // read moves above them (compiler fence), so at most two rows' values are live: a spill
-        // reload here would wait for vmcnt(0), i.e. for the ring's in-flight loads
-        const int ll = lane_id();                 // (recomputed: not worth a register)
-        double xn = my[rc * kDimTile + ll];
-        double xdn = DLY ? my[rd * kDimTile + ll] : sh;
+      if (tau + (int64_t)a.C * a.R < a.NT) {         // the next tile's first rows
+        rs_n = tile_rsrc(j0 + jstep, voff_n);
 #pragma unroll
-        for (int i = 0; i < TW; ++i) {
-          const double x = xn, xd = xdn;
-          if (i + 1 < TW && (PLAIN || i + 1 < rem)) {
-            xn = my[(rc + i + 1) * kDimTile + ll];
-            xdn = DLY ? my[(rd + i + 1) * kDimTile + ll] : sh;
+        for (int p = 0; p < PF; ++p)
+          xn[p] = __builtin_bit_cast(double,
+                                     __builtin_amdgcn_raw_buffer_load_b64(rs_n, voff_n, (p < n ? p : n - 1) * a.rowb, 0));
+      }
+      auto ldb = [&](int boff) -> double {         // sample at byte offset boff of the series
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, boff, 0));
+      };
+      auto ld = [&](int row) -> double { return ldb(row * a.rowb); };
+      // the rolling prefetch's next row, as a running byte offset (a scalar the compiler may not
+      // precompute per unrolled row: those products spilled the scalar file), clamped to row n - 1
+      const int last_off = (n - 1) * a.rowb;
+      const int dly_off = gofs * a.rowb;
+      int nxt = PF * a.rowb;
+      auto next_off = [&]() {
+        int o = nxt < last_off ? nxt : last_off;
+        asm volatile("" : "+s"(o));
+        nxt += a.rowb;
+        asm volatile("" : "+s"(nxt));
+        return o;
+      };
+      const double sh = xq[0];                      // row 0
+      const double sh2 = 2.0 * sh;
+      double ring[TL];
+#pragma unroll
+      for (int k = 0; k < TL; ++k) ring[k] = 0.0;
+      double s1 = 0.0, s2 = 0.0, r1 = 0.0, q4 = 0.0;
+      if constexpr (!Z) {
+        // rows 0 .. gofs - 1 (gofs >= PF, a multiple of PF): squares only; the rolling prefetch
+        // runs on into loop B's first rows (slot = row % PF = (row - gofs) % PF)
+        for (int s0 = 0; s0 < gofs; s0 += PF) {
+#pragma unroll
+          for (int p = 0; p < PF; ++p) {
+            const double y = xq[p] - sh;
+            s2 = __builtin_fma(y, y, s2);
+            xq[p] = ldb(next_off());                 // row s0 + p + PF
           }
-          asm volatile("" ::: "memory");
-          if (PLAIN || i < rem) {
+        }
+      }
+      const int nrow = n - gofs;                   // rows of loop B (>= 2)
+      // TL rows from row gofs + ci TL.  FIRST: chunk 0 (ramp, P events); MOM: moments; DLY: the
+      // delayed stream is a second load; RAG: fewer than TL rows left (uniform row tests)
+      auto chunk = [&](auto first_c, auto mom_c, auto dly_c, auto rag_c, int ci) {
+        constexpr bool FIRST = decltype(first_c)::value, MOM = decltype(mom_c)::value;
+        constexpr bool DLY = decltype(dly_c)::value, RAG = decltype(rag_c)::value;
+        const int s0 = gofs + ci * TL;
+        const int rem = n - s0;
+        auto row = [&](auto i_c) {
+          constexpr int i = decltype(i_c)::value;
+          // the loads are unconditional (rows past n re-read row n - 1): a load inside the ragged
+          // rows' branch made its register a phi whose copy waited for vmcnt(0) every row
+          const double x = xq[i % PF];
+          const double xd = DLY ? xdq[i % PF] : x;
+          {
+            const int o = next_off();                // row min(s0 + i + PF, n - 1)
+            xq[i % PF] = ldb(o);
+            if (DLY) xdq[i % PF] = ldb(o - dly_off);
+          }
+          // ragged rows past n: a uniform branch over the arithmetic only (the loads above are
+          // unconditional, so no load result is a phi: the waitcnt pass keeps its counts)
+          if (!RAG || i < rem) {
             const double y = x - sh;
             if constexpr (MOM) {
               r1 += x;
@@ -436,87 +356,131 @@ __global__ __launch_bounds__(64 * conv_waves(G), conv_wpe(TW, G)) void k_conv_ld
             }
             s2 = __builtin_fma(y, y, s2);
 #pragma unroll
-            for (int k = 0; k < TW; ++k) v[k] = __builtin_fma(y, ring[(i - 1 - k) & (TW - 1)], v[k]);
-            if constexpr (EV & 1) v[i] -= s2;
-            if constexpr (EV & 2) {
-              if (i == isuf) sufb = s2;
+            for (int k = 0; k < TL; ++k) {
+              if (FIRST && k >= i) continue;       // the ramp: slot (i - 1 - k) not written yet
+              v[k] = __builtin_fma(y, ring[(i - 1 - k + TL) % TL], v[k]);
             }
-            ring[i] = __builtin_fma(-2.0, xd, sh2);   // -2 (xd - sh), one rounding: exact scaling
+            if constexpr (FIRST) v[i] -= s2;       // P(gofs + 1 + i)
+            const double rv = __builtin_fma(-2.0, xd, sh2);   // -2 (xd - sh): exact scaling
+            if constexpr (DLY) q4 = __builtin_fma(rv, rv, q4);   // 4 x the delayed stream's squares
+            ring[i] = rv;
           }
-        }
-      };
-      const bool suf = isuf >= 0 && isuf < TW;
-      const bool plain = rem >= TW && !hwin && !suf;
-      // dly and the chunk's events as template arguments: g is not wave-uniform to the compiler,
-      // so runtime flags made every delayed read an exec-masked branch (a default move and mask
-      // saves per row) and every row of an event chunk two selects
-      auto go = [&](auto mom_c, auto dly_c) {
-        if (plain) {
-          rows(std::true_type{}, mom_c, dly_c, std::integral_constant<int, 0>{});
-        } else {
-          auto f = [&](auto ev_c) { rows(std::false_type{}, mom_c, dly_c, ev_c); };
-          static_dispatch<4>((hwin ? 1 : 0) | (suf ? 2 : 0), f);
-        }
-      };
-      if (g == 0) go(std::true_type{}, std::true_type{});   // g = 0: dly always
-      else if (dly) go(std::false_type{}, std::true_type{});
-      else go(std::false_type{}, std::false_type{});
-      if (cc == nch - 1) {                        // the split chain is complete
-        // q4 = 4 (S2 - S2 through n-1-gofs) + sum of the ring's (-2 y)^2: 4x the T_t suffix sums,
-        // exactly (power-of-2 scalings commute with rounding)
-        double q4 = 4.0 * (pos_suf >= 0 ? s2 - sufb : s2);
-        const double s2x2 = 2.0 * s2;
-        // the k-th latest delayed value sits in slot (n - 1 - k) mod TW: one static rotation per n
-        auto fin = [&](auto rl_c) {
-          constexpr int RL = decltype(rl_c)::value;
-#pragma unroll
-          for (int k = 0; k < TW; ++k) {
-            const double rk = ring[(RL - k) & (TW - 1)];
-            q4 = __builtin_fma(rk, rk, q4);
-            v[k] += __builtin_fma(-0.25, q4, s2x2);
-          }
+          // rows stay in program order: hoisting later rows' loads (the scheduler's choice in a
+          // straight-line chunk) holds their results in registers and spills the ring
+          __builtin_amdgcn_sched_barrier(0);
         };
-        static_dispatch<TW>((n - 1) & (TW - 1), fin);
-        if (g == 0) {
-          int nn = n;
-          asm volatile("" : "+s"(nn));            // n's doubles: converted here, not kept in registers
-          const double dn = nn;
-          const double mean = r1 / dn;
-          const double dm = mean - sh;
-          const double mm2 = (s2 - 2.0 * dm * s1) + dn * (dm * dm);
-          a_std += sqrt(mm2 > 0.0 ? mm2 / (dn - 1.0) : 0.0);
-          const double e = mean - S;
-          a_m += e;
-          a_m2 = __builtin_fma(e, e, a_m2);
-          const double yl = my[(rc + rem - 1) * kDimTile + lane_id()] - sh;   // lag n - 1: (x[n-1] - x[0])^2
-          a_last = __builtin_fma(yl, yl, a_last);
+        static_for<TL>(row);
+      };
+      auto run = [&](auto mom_c, auto dly_c) {
+        if (nrow < TL) chunk(std::true_type{}, mom_c, dly_c, std::true_type{}, 0);
+        else chunk(std::true_type{}, mom_c, dly_c, std::false_type{}, 0);
+        int ci = 1;
+        for (; (ci + 1) * TL <= nrow; ++ci) chunk(std::false_type{}, mom_c, dly_c, std::false_type{}, ci);
+        if (ci * TL < nrow) chunk(std::false_type{}, mom_c, dly_c, std::true_type{}, ci);
+      };
+      if constexpr (Z) run(std::true_type{}, std::false_type{});   // (moments unused unless mom)
+      else run(std::false_type{}, std::true_type{});
+      // Q(t) = S2 - P(n - t), t = gofs + 1 + k: 4 (S2 - P(n - gofs)) (0 for gofs = 0), plus the
+      // squares of the last k + 1 delayed samples, slot (n - 1 - gofs - k') mod TL, k' <= k
+      double q = Z ? 0.0 : 4.0 * s2 - q4;
+      const double s2x2 = 2.0 * s2;
+      auto fin = [&](auto rl_c) {
+        constexpr int RL = decltype(rl_c)::value;
+#pragma unroll
+        for (int k = 0; k < TL; ++k) {
+          const double rk = ring[(RL - k + TL) % TL];
+          q = __builtin_fma(rk, rk, q);            // 4 Q(gofs + 1 + k)
+          v[k] += __builtin_fma(-0.25, q, s2x2);
         }
+      };
+      static_dispatch<TL>((n - 1 - gofs) % TL, fin);
+      if (mom && valid) {
+        const double dn = n;
+        const double mean = r1 / dn;
+        const double dm = mean - sh;
+        const double mm2 = (s2 - 2.0 * dm * s1) + dn * (dm * dm);
+        a_std += sqrt(mm2 > 0.0 ? mm2 / (dn - 1.0) : 0.0);
+        const double e = mean - Sd;
+        a_m += e;
+        a_m2 = __builtin_fma(e, e, a_m2);
+        const double yl = ld(n - 1) - sh;          // lag n - 1: (x[n-1] - x[0])^2
+        a_last = __builtin_fma(yl, yl, a_last);
       }
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();                                // every wave is done with the ring
-  double* const red = ring_x;                     // [NW][kDimTile]
-  auto put = [&](int row, double x) {
-    red[w * kDimTile + dl] = x;
-    __syncthreads();
-    if (w == 0 && d < s.D && grp < groups) {
-      double acc = red[dl];
+  double* out = partial + (int64_t)W * kLagRows * 64 + lane;
+  out[0] = a_std;
+  out[64] = a_m;
+  out[128] = a_m2;
+  out[192] = a_last;
 #pragma unroll
-      for (int ww = 1; ww < NW; ++ww) acc += red[ww * kDimTile + dl];
-      partial[((int64_t)grp * (T + 4) + row) * s.D + d] = acc;
-    }
-    __syncthreads();
-  };
-  put(0, g == 0 ? a_std : 0.0);
-  put(1, g == 0 ? a_m : 0.0);
-  put(2, g == 0 ? a_m2 : 0.0);
-#pragma unroll
-  for (int gg = 0; gg < G; ++gg) {
-#pragma unroll
-    for (int k = 0; k < TW; ++k) put(3 + gg * TW + k, g == gg && gg * TW + k + 1 < s.n ? v[k] : 0.0);   // lags t >= n: 0
+  for (int k = 0; k < TL; ++k) out[(4 + k) * 64] = v[k];
+}
+
+template <int TL, int PF>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_LAG_WPE, HMC_LAG_WPE))) void k_conv_series(LagArgs a,
+                                                                                               double* partial) {
+  const int W = blockIdx.x;
+  const int u = W >> 3;
+  const int g = u % a.G;
+  const int cr = (u / a.G) * 8 + (W & 7);
+  const int c = cr % a.C, r = cr / a.C;
+  if (r >= a.R) return;                            // grid padding (never reduced)
+  if (a.L0 + g * TL == 0) lag_wave<TL, PF, true>(a, W, g, c, r, partial);
+  else lag_wave<TL, PF, false>(a, W, g, c, r, partial);
+}
+
+// inter[(c * G + g) * kLagRows + row][l] = sum over the replicas r (in order) of the waves' lanes
+__global__ __launch_bounds__(256) void k_lag_classes(LagArgs a, const double* __restrict__ partial,
+                                                     double* __restrict__ inter) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tot = (int64_t)a.C * a.G * kLagRows * 64;
+  if (i >= tot) return;
+  const int l = (int)(i & 63);
+  const int64_t cgr = i >> 6;
+  const int row = (int)(cgr % kLagRows);
+  const int64_t cg = cgr / kLagRows;
+  const int g = (int)(cg % a.G), c = (int)(cg / a.G);
+  double acc = 0.0;
+  for (int r = 0; r < a.R; ++r) {
+    const int cr = r * a.C + c;
+    const int64_t W = 8 * (g + (int64_t)a.G * (cr / 8)) + (cr & 7);
+    acc += partial[(W * kLagRows + row) * 64 + l];
   }
-  put(3 + T, g == 0 && s.n >= 2 ? a_last : 0.0);  // lag n - 1 (the ESS loop's last), whatever T
+  inter[i] = acc;
+}
+
+// out[orow][d]: conv layout (conv != 0: rows std, mean - S, (mean - S)^2, lags L0 + 1 + skip ..,
+// lag n - 1; nlag lags) or lags only; lags t >= n are 0.  Sums the classes' lanes that hold
+// dimension d, in a fixed order.
+__global__ __launch_bounds__(256) void k_lag_dims(LagArgs a, const double* __restrict__ inter, int conv, int skip,
+                                                  int nlag, double* __restrict__ out) {
+  const int D = a.s.D;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nrow = conv ? nlag + 4 : nlag;
+  if (i >= (int64_t)nrow * D) return;
+  const int orow = (int)(i / D), d = (int)(i - (int64_t)orow * D);
+  int g = 0, prow;
+  int t = 0;                                       // lag (0: a moment row)
+  if (conv && orow < 3) prow = orow;
+  else if (conv && orow == nlag + 3) {
+    prow = 3;
+    t = a.s.n - 1;
+  } else {
+    const int k = skip + orow - (conv ? 3 : 0);    // lag index inside the pass
+    g = k / kLagTL;
+    prow = 4 + k % kLagTL;
+    t = a.L0 + 1 + k;
+  }
+  double acc = 0.0;
+  if (t < a.s.n && !(conv && orow == nlag + 3 && a.s.n < 2)) {
+    for (int c = 0; c < a.C; ++c) {
+      int l = (int)(((int64_t)d - 64 * (int64_t)c) % D);
+      if (l < 0) l += D;
+      for (; l < 64; l += D) acc += inter[(((int64_t)c * a.G + g) * kLagRows + prow) * 64 + l];
+    }
+  }
+  out[i] = acc;
 }
 
 // ---- streaming (windowed) split-chain statistics: q_chain never has to be stored whole.
@@ -690,28 +654,198 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T <= 16 ? 3
   }
 }
 
-int64_t rows_chunks(int64_t rows) { return (rows + kRowChunk - 1) / kRowChunk; }
-
-// Blocks resident per CU for the lag kernel of T lags (LDS ring and VGPRs; see the launch switch).
-#ifdef HMC_CONV48_BPC3   // A/B: 48-lag grid sized for 3 blocks per CU
-constexpr int conv_blocks_per_cu(int T) { return T == 16 ? 1 : T == 32 ? 2 : 3; }
-#else
-constexpr int conv_blocks_per_cu(int T) { return T == 16 ? 1 : T == 32 ? 2 : T == 48 ? 4 : 3; }
-#endif
-
-// Block groups of the lag pass: one resident wave of blocks over all dim tiles (no tail wave).
-int64_t conv_groups(int64_t n_chains, int D, int T) {
-  const int64_t g = (2 * n_chains + 3) / 4;       // 4 split chains per block row set
-  const int ntiles = (D + kDimTile - 1) / kDimTile;
-  int64_t cap = (int64_t)256 * conv_blocks_per_cu(T) / ntiles;
-  cap = cap >= 8 ? cap / 8 * 8 : 8;
-  return g < cap ? (g < 1 ? 1 : g) : cap;
+// The product form (halves of n >= T samples) as its own kernel, T rows per unrolled chunk so that
+// every ring slot is a static register: position p lives in slot p mod T (chunks start at
+// multiples of T), so the lag products, the ring update and both per-half events (H_t at half
+// position T-1, T_t at n-1) index the ring statically -- no ring shifts (T moves per row before).
+// Rows arrive by a rolling prefetch (slot p mod PF; the load of row p + PF is issued as row p is
+// consumed), so PF rows per wave are always in flight instead of one chunk at a time; a wave's rows
+// are one chain's (buffer descriptor on the chain, row offsets in the scalar offset).  Same sums
+// in the same order as the difference-form kernel's PROD path had: bit-identical results.
+template <int T>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T <= 16 ? 3 : 1))) void k_stream_prod(StreamArgs a) {
+  constexpr int PF = 8;
+  static_assert(T % PF == 0, "prefetch slots repeat per chunk");
+  __shared__ double red[4][kDimTile];
+  const int dl = threadIdx.x & (kDimTile - 1);
+  const int rl = __builtin_amdgcn_readfirstlane(threadIdx.x / kDimTile);   // wave-uniform: one chain per wave
+  const int d = blockIdx.y * kDimTile + dl;
+  const int dd = d < a.D ? d : a.D - 1;            // lanes past D load a valid element, write nothing
+  const int64_t left = 2 * (int64_t)a.n - a.pos0;
+  const int rows = (int)(left < a.rows ? (left > 0 ? left : 0) : a.rows);
+  const int64_t pos0 = a.pos0, pend = a.pos0 + rows;
+  double v[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) v[t] = 0.0;
+  for (int64_t c = (int64_t)blockIdx.x * 4 + rl; c < a.n_chains; c += (int64_t)a.groups * 4) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<double*>(a.x + c * a.chain_stride), 0, -1, 0x00020000);
+    auto at = [&](int k) -> double {                // k-th window sample (k < carry + rows)
+      int sl = a.slot0 + k;
+      sl = sl >= a.wrap ? sl - a.wrap : sl;
+      return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                            rs, dd * 8, (int)(sl * a.sample_stride * 8), 0));
+    };
+    auto kpos = [&](int64_t p) { return (int)(a.carry + (p - pos0)); };
+    const int64_t o = c * 2 * a.D + dd;
+    const int hc = pos0 >= a.n ? 1 : 0;
+    // the current half's shift and sums; the other half's as stored
+    double csh = a.shift[o + hc * a.D], cm1 = a.s1[o + hc * a.D], cm2 = a.s2[o + hc * a.D];
+    double sh0 = a.shift[o], m10 = a.s1[o], m20 = a.s2[o];
+    const double sh1s = a.shift[o + a.D], m11s = a.s1[o + a.D], m21s = a.s2[o + a.D];
+    const int sidx0 = (int)(pos0 - (int64_t)hc * a.n);
+    // ring: carry samples of the same half, slot = position mod T
+    const int lim = a.carry < sidx0 ? a.carry : sidx0;
+    double ring[T];
+#pragma unroll
+    for (int sl = 0; sl < T; ++sl) {
+      const int k = (int)(((pos0 - 1 - sl) % T + T) % T);   // pos0 - 1 - k = position in slot sl
+      const int kk = a.carry - 1 - k;
+      ring[sl] = at(kk > 0 ? kk : 0);               // unconditional, all issued before any use
+    }
+    __builtin_amdgcn_sched_barrier(0);              // (the scheduler serialised load -> use pairs)
+#pragma unroll
+    for (int sl = 0; sl < T; ++sl) {
+      const int k = (int)(((pos0 - 1 - sl) % T + T) % T);
+      ring[sl] = k < lim ? ring[sl] - csh : 0.0;
+    }
+    double xs[PF];
+#pragma unroll
+    for (int sl = 0; sl < PF; ++sl) {
+      const int64_t p = pos0 + (((sl - pos0) % PF) + PF) % PF;   // the first row with p = sl mod PF
+      xs[sl] = at(kpos(p < pend ? p : pos0));       // (unconditional: rows past the end are unused)
+    }
+    int nsl = (a.slot0 + kpos(pos0 + PF)) % a.wrap;   // window slot of the next row to prefetch
+    const int64_t P0 = pos0 - ((pos0 % T) + T) % T;
+    for (int64_t pc = P0; pc < pend; pc += T) {
+      auto row = [&](auto j_c) {
+        constexpr int j = decltype(j_c)::value;
+        const int64_t p = pc + j;
+        if (p >= pos0 && p < pend) {                  // uniform
+          const double x = xs[j % PF];
+          if (p + PF < pend) {                        // row p + PF: a running window slot (scalar;
+            int sl = nsl;                             // precomputed per unrolled row they spilled)
+            asm volatile("" : "+s"(sl));
+            xs[j % PF] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                       rs, dd * 8, (int)(sl * a.sample_stride * 8), 0));
+            nsl = sl + 1 == a.wrap ? 0 : sl + 1;
+          }
+          if (p == a.n) {                            // the call crosses into half 1
+            sh0 = csh;
+            m10 = cm1;
+            m20 = cm2;
+            csh = sh1s;
+            cm1 = m11s;
+            cm2 = m21s;
+          }
+          const int sidx = (int)(p < a.n ? p : p - a.n);
+          if (sidx == 0) {                           // a half starts: its shift, an empty ring
+            csh = x;
+#pragma unroll
+            for (int k = 0; k < T; ++k) ring[k] = 0.0;
+          }
+          const double y = x - csh;
+          cm1 += y;
+          cm2 = __builtin_fma(y, y, cm2);
+          const double ym2 = -2.0 * y;
+#pragma unroll
+          for (int t = 0; t < T; ++t) v[t] = __builtin_fma(ym2, ring[(j - 1 - t + 2 * T) % T], v[t]);   // -2 C_t
+          ring[j] = y;
+          if (sidx == T - 1) {                       // the half's first T samples: H_t = sum_{s<t} y^2
+            double q = 0.0;
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+              const double r = ring[(j - (T - 1) + t + T) % T];
+              q = __builtin_fma(r, r, q);
+              v[t] -= q;
+            }
+          }
+          if (sidx == a.n - 1) {                     // its last T samples: T_t; then + 2 S2
+            double q = 0.0;
+            const double s2x2 = 2.0 * cm2;
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+              const double r = ring[(j - t + T) % T];
+              q = __builtin_fma(r, r, q);
+              v[t] += s2x2 - q;
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      static_for<T>(row);
+    }
+    if (d < a.D) {
+      const bool crossed = pos0 < a.n && pend > a.n;
+      if (hc == 1 || crossed) {
+        a.shift[o + a.D] = csh;
+        a.s1[o + a.D] = cm1;
+        a.s2[o + a.D] = cm2;
+      }
+      if (hc == 0) {
+        a.shift[o] = crossed ? sh0 : csh;
+        a.s1[o] = crossed ? m10 : cm1;
+        a.s2[o] = crossed ? m20 : cm2;
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    red[rl][dl] = v[t];
+    __syncthreads();
+    if (rl == 0 && d < a.D)
+      a.vpart[((int64_t)blockIdx.x * T + t) * a.D + d] = ((red[0][dl] + red[1][dl]) + red[2][dl]) + red[3][dl];
+    __syncthreads();
+  }
 }
 
-int64_t vario_jchunk(int64_t m2) {
-  // ~4096 blocks at most; at least 16 split chains per block
-  int64_t c = (m2 + 4095) / 4096;
-  return c < 16 ? 16 : c;
+int64_t rows_chunks(int64_t rows) { return (rows + kRowChunk - 1) / kRowChunk; }
+
+LagArgs lag_args(const Src& s, int L0, int T, int mom) {
+  LagArgs a{};
+  a.s = s;
+  a.L0 = L0;
+  a.T = T;
+  a.G = (T + kLagTL - 1) / kLagTL;
+  a.mom = mom;
+  a.C = s.D / lag_gcd(s.D, 64);
+  a.NT = (2 * s.n_chains * (int64_t)s.D + 63) / 64;
+  const int64_t per_class = (a.NT + a.C - 1) / a.C;
+  const int64_t R = (kLagWaves + (int64_t)a.C * a.G - 1) / ((int64_t)a.C * a.G);
+  a.R = (int)(R < per_class ? (R < 1 ? 1 : R) : per_class);
+  a.rowb = (int)(s.sample_stride * 8);
+  return a;
+}
+
+int64_t lag_grid(const LagArgs& a) { return 8 * (int64_t)a.G * (((int64_t)a.C * a.R + 7) / 8); }
+int64_t lag_work(const LagArgs& a) {
+  return lag_grid(a) * kLagRows * 64 + (int64_t)a.C * a.G * kLagRows * 64;
+}
+
+// One read of the samples: lags L0 + 1 .. L0 + T (group 0 also the moments when mom), reduced into
+// out (conv layout or lags only, from lag L0 + 1 + skip, nlag lags).
+hipError_t launch_lags(const Src& s, int L0, int T, int mom, int conv, int skip, int nlag, double* work, double* out,
+                       hipStream_t st) {
+  if (T < 1 || L0 < 0 || L0 % kLagPF != 0) return hipErrorInvalidValue;
+  // lane offsets (bytes from a tile's first split chain) and row offsets must stay inside the
+  // buffer bound: at most 64 / D + 2 split chains per tile; the second half of a chain starts
+  // n * sample_stride after its first (chain_stride >= that for every q_chain view)
+  const int64_t cs = s.chain_stride, ss = s.sample_stride;
+  if (cs < (int64_t)s.n * ss || ss < 1 || ss * 8 > 0x7FFFFFFF) return hipErrorInvalidValue;
+  const int64_t span = ((64 / s.D + 2) / 2 + 1) * cs + (int64_t)s.n * ss + s.D;   // doubles
+  if ((span + (int64_t)s.n * ss) * 8 >= kLagOOB) return hipErrorInvalidValue;
+  const LagArgs a = lag_args(s, L0, T, mom);
+  const int64_t grid = lag_grid(a);
+  double* partial = work;
+  double* inter = work + grid * kLagRows * 64;
+  k_conv_series<kLagTL, kLagPF><<<(unsigned)grid, 64, 0, st>>>(a, partial);
+  if (hipError_t e = hipGetLastError()) return e;
+  const int64_t ni = (int64_t)a.C * a.G * kLagRows * 64;
+  k_lag_classes<<<(unsigned)((ni + 255) / 256), 256, 0, st>>>(a, partial, inter);
+  if (hipError_t e = hipGetLastError()) return e;
+  const int64_t no = (int64_t)(conv ? nlag + 4 : nlag) * s.D;
+  k_lag_dims<<<(unsigned)((no + 255) / 256), 256, 0, st>>>(a, inter, conv, skip, nlag, out);
+  return hipGetLastError();
 }
 
 }  // namespace
@@ -719,9 +853,8 @@ int64_t vario_jchunk(int64_t m2) {
 int64_t diag_rowsum_work(int64_t rows, int D) { return rows_chunks(rows) * D; }
 
 int64_t diag_variogram_work(int64_t n_chains, int D, int nlags) {
-  const int64_t m2 = 2 * n_chains;
-  const int64_t jc = vario_jchunk(m2);
-  return ((m2 + jc - 1) / jc) * (int64_t)nlags * D;
+  Src s{nullptr, 0, 0, 0, n_chains, 2, D};
+  return lag_work(lag_args(s, 0, nlags + kLagPF - 1, 0));   // the lag range may start up to PF-1 lower
 }
 
 hipError_t launch_split_moments(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int64_t base, int n,
@@ -744,38 +877,15 @@ hipError_t launch_rowsum(const double* x, int64_t n_outer, int64_t os, int64_t n
   return hipGetLastError();
 }
 
-int64_t diag_conv_work(int64_t n_chains, int D, int T) { return conv_groups(n_chains, D, T) * (int64_t)(T + 4) * D; }
+int64_t diag_conv_work(int64_t n_chains, int D, int T) {
+  Src s{nullptr, 0, 0, 0, n_chains, 2, D};
+  return lag_work(lag_args(s, 0, T, 1));
+}
 
 hipError_t launch_conv_fused(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int64_t base, int n, int D,
                              int T, double* work, double* out, hipStream_t st) {
   Src s{x, cs, ss, base, n_chains, n, D};
-  const int64_t groups = conv_groups(n_chains, D, T);
-  const int ntiles = (D + kDimTile - 1) / kDimTile;
-  // blocks: 8 groups x ntiles per 8 * ntiles consecutive block ids (XCD-aware order, see kernel)
-  const int64_t gpad = (groups + 7) / 8 * 8;
-  const dim3 grid((unsigned)(gpad * ntiles));
-  // the direct-to-LDS loads move dim pairs of 16 B: rows must start 16-B aligned and hold whole pairs
-  if (((D | cs | ss | base) & 1) || (reinterpret_cast<uintptr_t>(x) & 15)) {
-    switch (T) {
-      case 8: k_conv_lags<8, 1><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
-      case 16: k_conv_lags<16, 1><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
-      case 32: k_conv_lags<16, 2><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
-      case 48: k_conv_lags<16, 3><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
-      case 64: k_conv_lags<16, 4><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
-      default: return hipErrorInvalidValue;
-    }
-  } else switch (T) {   // T = TW x G lags; rows staged through LDS by direct-to-LDS loads, 2 chunks ahead
-    case 8: k_conv_lds<8, 1, 2><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
-    case 16: k_conv_lds<16, 1, 2><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
-    case 32: k_conv_lds<16, 2, 2><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
-    case 48: k_conv_lds<16, 3, 2><<<grid, 192, 0, st>>>(s, (int)groups, ntiles, work); break;
-    case 64: k_conv_lds<16, 4, 2><<<grid, 256, 0, st>>>(s, (int)groups, ntiles, work); break;
-    default: return hipErrorInvalidValue;
-  }
-  if (hipError_t e = hipGetLastError()) return e;
-  const int64_t ncols = (int64_t)(T + 4) * D;
-  k_colsum_final<<<(unsigned)((ncols + 255) / 256), 256, 0, st>>>(work, groups, ncols, out);
-  return hipGetLastError();
+  return launch_lags(s, 0, T, 1, 1, 0, T, work, out, st);
 }
 
 int64_t diag_stream_groups(int64_t n_chains) {
@@ -786,6 +896,7 @@ int64_t diag_stream_groups(int64_t n_chains) {
 hipError_t launch_stream_accum(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int D, int wrap, int slot0,
                                int carry, int rows, int64_t pos0, int n, double* shift, double* s1, double* s2, int T,
                                double* vpart, double* vsum, hipStream_t st) {
+  if ((int64_t)wrap * ss * 8 >= 0x7FFFFFFF) return hipErrorInvalidValue;   // row offsets: 32-bit scalar offsets
   const int64_t groups = diag_stream_groups(n_chains);
   StreamArgs a{x, n_chains, cs, ss, D, wrap, slot0, carry, rows, n, pos0, shift, s1, s2, vpart, (int)groups};
   dim3 grid((unsigned)groups, (unsigned)((D + kDimTile - 1) / kDimTile));
@@ -794,7 +905,7 @@ hipError_t launch_stream_accum(const double* x, int64_t n_chains, int64_t cs, in
   const bool prod = n >= T;
   auto go = [&](auto t_c) {
     constexpr int TT = decltype(t_c)::value;
-    if (prod) k_stream_accum<TT, true><<<grid, 256, 0, st>>>(a);
+    if (prod) k_stream_prod<TT><<<grid, 256, 0, st>>>(a);
     else k_stream_accum<TT, false><<<grid, 256, 0, st>>>(a);
   };
   switch (T) {
@@ -813,23 +924,8 @@ hipError_t launch_stream_accum(const double* x, int64_t n_chains, int64_t cs, in
 hipError_t launch_variogram(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int64_t base, int n, int D,
                             int t0, int t1, double* work, double* out, hipStream_t st) {
   Src s{x, cs, ss, base, n_chains, n, D};
-  const int64_t m2 = 2 * n_chains;
-  const int64_t jc = vario_jchunk(m2);
-  const int64_t nch = (m2 + jc - 1) / jc;
-  dim3 grid((unsigned)nch, (unsigned)((D + kDimTile - 1) / kDimTile));
-  // lags in blocks of <= 32 per pass; work holds [nch][t1 - t0][D] partials
-  for (int a = t0; a < t1; a += 32) {
-    const int nt = t1 - a < 32 ? t1 - a : 32;
-    double* part = work + (int64_t)nch * (a - t0) * D;
-    if (nt <= 8) k_variogram_ring<8><<<grid, 256, 0, st>>>(s, a, nt, jc, part);
-    else if (nt <= 16) k_variogram_ring<16><<<grid, 256, 0, st>>>(s, a, nt, jc, part);
-    else k_variogram_ring<32><<<grid, 256, 0, st>>>(s, a, nt, jc, part);
-    if (hipError_t e = hipGetLastError()) return e;
-    const int64_t ncols = (int64_t)nt * D;
-    k_colsum_final<<<(unsigned)((ncols + 255) / 256), 256, 0, st>>>(part, nch, ncols, out + (int64_t)(a - t0) * D);
-    if (hipError_t e = hipGetLastError()) return e;
-  }
-  return hipSuccess;
+  const int L0 = (t0 - 1) / kLagPF * kLagPF;   // the pass starts at a prefetch-aligned lag
+  return launch_lags(s, L0, t1 - 1 - L0, 0, 0, t0 - 1 - L0, t1 - t0, work, out, st);
 }
 
 }  // namespace hmc

@@ -130,7 +130,9 @@ __host__ __device__ inline size_t nuts_queue_bytes(int64_t n) { return (size_t)(
 // the whole wave waited for at every tree end (profiles/r03_c5_nuts_phases.json), and the tree
 // kernel needs no Box-Muller tables in LDS.  Longer ranges run as several launches.
 constexpr int kNutsMomIters = 32;
-__host__ __device__ inline int64_t nuts_mom_doubles(int64_t n, int MT) { return n * kNutsMomIters * 4 * MT * 4; }
+__host__ __device__ inline int64_t nuts_mom_doubles(int64_t n, int MT, int iters) {
+  return n * (iters < kNutsMomIters ? iters : kNutsMomIters) * 4 * MT * 4;
+}
 
 // Workspace: per chain slot, nvec vectors of Dp = 4M doubles (dims, zero padded), slot-contiguous,
 // the 16 slots of a wave in one block addressed through a wave-uniform buffer descriptor (SGPR
@@ -252,10 +254,12 @@ __device__ __forceinline__ double mac(double acc, double x, double y) {
   else return __builtin_fma(x, y, acc);
 }
 
-// Momenta of iterations [it0, it1) (it1 - it0 <= kNutsMomIters) for every chain: p ~ N(0, cov_p)
+// Momenta of iterations [it0, it1) (K = it1 - it0 <= kNutsMomIters) for every chain: p ~ N(0, cov_p)
 // with a diagonal cov_p (samplers.py:565, :829), exactly the tree kernel's former in-kernel draws
 // (pair slot h + 4m -> dims h + 4m and h + 4m + 4, table Box-Muller, pscale, zero padding).
-// Layout: per (chain, iteration) one 4M-double vector in the workspace's pair layout (ws_elem):
+// Layout: per (chain, iteration) one 4M-double vector, chain-major (c * K + it - it0; the buffer holds
+// min(kNutsMomIters, iterations per call) iterations, hmc_nuts_workspace_size_ex), in the
+// workspace's pair layout (ws_elem):
 // 16-byte slot s = 4j + h holds dims (h + 8j, h + 8j + 4), so slot s sits at doubles 2s..2s+1 and
 // consecutive threads write consecutive 16-byte slots.
 template <int MT, bool GEN>
@@ -282,7 +286,7 @@ __global__ __launch_bounds__(256) void k_nuts_momenta(RandArgs a, double* __rest
     }
     z0 = d0 < a.D ? z0 : 0.0;
     z1 = d1 < a.D ? z1 : 0.0;
-    *reinterpret_cast<double2*>(pm + (c * kNutsMomIters + (vec - c * K)) * (4 * M) + 2 * r) = make_double2(z0, z1);
+    *reinterpret_cast<double2*>(pm + (c * K + (vec - c * K)) * (4 * M) + 2 * r) = make_double2(z0, z1);
   }
 }
 
@@ -406,8 +410,8 @@ void k_nuts_iters(RandArgs a) {
         if (state == S_FETCH) live = false;
       }
       NUTS_SUBPHASE(9);
-      {                                                 // next unit from the queue (converged shuffle)
-        const bool fetching = state == S_FETCH;
+      if (__builtin_amdgcn_ballot_w64(state == S_FETCH)) {   // next unit from the queue (converged shuffle;
+        const bool fetching = state == S_FETCH;              // skipped in the steps where no slot fetches)
         unsigned long long u = (fetching && h == 0) ? atomicAdd(queue, 1ull) : 0ull;
         u = __shfl(u, lane & 15, kWave);
         if (fetching) {
@@ -448,7 +452,7 @@ void k_nuts_iters(RandArgs a) {
           Eprev = ld_wt_d(a.Eprev + c);
           tpos = REPLAY ? ld_wt(tcur + c) : 0;
           if constexpr (PG) {                           // this iteration's momentum, with the state
-            const double* pv = pm + (c * kNutsMomIters + (it - a.it0)) * (4 * M) + 2 * h;
+            const double* pv = pm + (c * (a.it1 - a.it0) + (it - a.it0)) * (4 * M) + 2 * h;
 #pragma unroll
             for (int m = 0; m < M; m += 2) {
               const double2 z = *reinterpret_cast<const double2*>(pv + 4 * m);
@@ -924,12 +928,13 @@ hipError_t launch_nuts_mt(const RandArgs& a, bool exact, bool gen, bool replay, 
 
 }  // namespace
 
-int64_t nuts_ws_doubles(int64_t n, int D, int d_max) {
+int64_t nuts_ws_doubles(int64_t n, int D, int d_max, int mom_iters) {
   const int MT = dense_tiles(D);
   const int64_t waves = (n + 15) / 16;
-  // vectors + tape cursors + work queue (head, spare, per-chain iterations done) + momenta
+  // vectors + tape cursors + work queue (head, spare, per-chain iterations done) + the Philox
+  // momenta drawn ahead (diagonal cov_p only) for min(32, iterations per call) iterations
   return waves * (int64_t)(V_SLOTS + 2 * (d_max + 1)) * 4 * MT * kWave + waves * 16 + nuts_queue_bytes(n) / 8 +
-         nuts_mom_doubles(n, MT);
+         nuts_mom_doubles(n, MT, mom_iters);
 }
 
 #ifdef HMC_NUTS_DEV_C5

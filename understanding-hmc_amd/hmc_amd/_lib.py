@@ -66,6 +66,8 @@ SYMBOLS = {
                                              c_dp, c_dp]),
     "hmc_random_workspace_size": (ctypes.c_int64, [ctypes.POINTER(Target), ctypes.c_int64]),
     "hmc_nuts_workspace_size": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32]),
+    "hmc_nuts_workspace_size_ex": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                                    ctypes.c_int32]),
     "hmc_nuts_iters": (ctypes.c_int, [ctypes.POINTER(Target), ctypes.POINTER(Kinetic), ctypes.POINTER(Schedule),
                                       ctypes.POINTER(Replay), ctypes.POINTER(State), c_dp, c_dp]),
     "hmc_leapfrog": (ctypes.c_int, [ctypes.POINTER(Target), ctypes.POINTER(Kinetic), ctypes.c_int64, c_dp, c_dp,

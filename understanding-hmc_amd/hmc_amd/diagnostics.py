@@ -15,9 +15,6 @@ import torch
 
 from . import _lib as H
 
-_LAG_BLOCK = 32
-
-
 def _as_device(x):
     """(Nchain, T, D) float64 CUDA tensor view (no copy when already on the device)."""
     if isinstance(x, torch.Tensor):
@@ -109,15 +106,17 @@ def convergence_sums(sp, tmax):
     return out
 
 
-_TMAX = (8, 16, 32, 48, 64)
+FIRST_PASS_LAGS = 96
 
 
 def conv_tmax(n):
-    """Lag groups of the one-pass sums for split chains of n samples: lags 1..tmax, tmax the
-    smallest width >= n - 2, since the pass always adds lag n - 1 (one square per split chain), so
-    every lag t < n is there when n <= 66 (n = 50, the bench window: 48 lags, three waves per split
-    chain instead of four)."""
-    return next((t for t in _TMAX if t >= n - 2), _TMAX[-1])
+    """Lags 1..tmax of the one-pass sums for split chains of n samples.  The pass always adds lag
+    n - 1 (one square per split chain), so tmax = n - 2 makes it complete: every lag t < n, the
+    whole ESS loop, in one read of the samples (n = 50, the bench window: 48 lags).  Longer chains
+    take the first FIRST_PASS_LAGS lags; dimensions whose criterion has not fired by then read
+    all the remaining lags in ONE more pass (hmc_variogram), so a slow-mixing window is read at
+    most twice and a fast-mixing one once, without the O(n^2) cost of every lag."""
+    return max(1, min(n - 2, FIRST_PASS_LAGS))
 
 
 def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
@@ -125,10 +124,10 @@ def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
     (views such as q_chain_device[:, 1:, :] are read in place).  Returns (R, n_eff) NumPy.
 
     One pass over the samples gives every per-dimension sum R-hat needs and the variogram of every
-    lag t < n up to 64, and of lag n - 1 (hmc_convergence_sums); the ESS termination
+    lag t < n up to conv_tmax(n), and of lag n - 1 (hmc_convergence_sums); the ESS termination
     (utils.py:130-157) runs vectorised over the dimensions on the host, and only dimensions whose
-    criterion has not fired by then (n > 66 and slow mixing) read further lag blocks
-    (hmc_variogram).  Ranks all-reduce the per-dimension sums: two rounds, B needs the global
+    criterion has not fired by then (n > 98 and slow mixing) read the remaining lags, all in one
+    more pass (hmc_variogram).  Ranks all-reduce the per-dimension sums: two rounds, B needs the global
     mean."""
     sp = _Split(q_chain, thin_rate, warm_up_num)
     n, D = sp.n, sp.D
@@ -178,16 +177,13 @@ def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
             ssp = sp
             idx = np.arange(D)
         Vs = Vt[:, idx]
-        while True:
-            t0 = Vs.shape[0] + 1
-            t1 = min(t0 + _LAG_BLOCK, lmax + 1)
-            vb = _allreduce(variogram_sums(ssp, t0, t1), group).cpu().numpy()
-            LAST_INFO["fallback_passes"] += 1
-            lags = np.arange(t0, t1)
-            Vs = np.vstack([Vs, vb / (m * (n - lags))[:, None]])
-            ne, need2 = ess_vectorised(Vs, var_h[idx], n, m, complete=Vs.shape[0] >= lmax)
-            if not need2.any():
-                break
+        t0, t1 = Vs.shape[0] + 1, lmax + 1                              # every remaining lag t < n
+        vb = _allreduce(variogram_sums(ssp, t0, t1), group).cpu().numpy()
+        LAST_INFO["fallback_passes"] += 1
+        lags = np.arange(t0, t1)
+        Vs = np.vstack([Vs, vb / (m * (n - lags))[:, None]])
+        ne, need2 = ess_vectorised(Vs, var_h[idx], n, m, complete=True)
+        assert not need2.any()
         n_eff[idx] = ne
         LAST_INFO["lags"] = Vs.shape[0]
     return R.cpu().numpy(), n_eff

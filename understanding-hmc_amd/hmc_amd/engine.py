@@ -260,7 +260,7 @@ class NutsEngine(RandomEngine):
 
     def __init__(self, target, n_chains, n_iter, warm_up, thin, d_max, dt, cov_p=None, rng="philox", seed=0,
                  fp_mode="fast", chain_offset=0, store_chain=True, store_energy=True, on_dmax="raise",
-                 device=None):
+                 device=None, iters_per_call=None):
         # order_tiles=False: the NUTS kernel uses neither the tile order nor the gradient cache
         super().__init__(target, n_chains, n_iter, warm_up, thin, 5, 20, dt, cov_p=cov_p, rng=rng, seed=seed,
                          fp_mode=fp_mode, chain_offset=chain_offset, store_chain=store_chain,
@@ -271,7 +271,12 @@ class NutsEngine(RandomEngine):
         self.on_dmax = 0 if on_dmax == "raise" else 1
         if self.D > 128 and self._minv_full is not None:
             raise NotImplementedError("NUTS with a full cov_p: D=%d not supported (D <= 128)" % self.D)
-        nbytes = H.lib().hmc_nuts_workspace_size(self.D, self.N, self.d_max)
+        # the Philox momenta drawn ahead are sized for the longest run() call (at most 32 iterations
+        # are drawn per launch); replay tapes and a full cov_p draw in the kernel and need none
+        self.iters_per_call = int(iters_per_call or n_iter)
+        philox_mom = int(rng == "philox" and self._minv_full is None)
+        nbytes = H.lib().hmc_nuts_workspace_size_ex(self.D, self.N, self.d_max, max(1, self.iters_per_call),
+                                                    philox_mom)
         if nbytes <= 0:
             raise NotImplementedError("NUTS kernel: d_max=%d not supported (1 <= d_max <= 15)" % self.d_max)
         self.ws = torch.zeros((nbytes + 7) // 8, dtype=torch.float64, device=self.device)
@@ -285,5 +290,6 @@ class NutsEngine(RandomEngine):
                                 H.ptr(self._streams[2]), tape.shape[1])
 
     def run(self, it0, it1):
+        assert it1 - it0 <= self.iters_per_call, "NutsEngine.run: more iterations than iters_per_call"
         H.check(H.lib().hmc_nuts_iters(self.T, self.K, self.schedule(it0, it1), self._replay, self.S,
                                        H.ptr(self.ws), self.stream()), "hmc_nuts_iters")

@@ -342,7 +342,9 @@ class HMC_sampler(sampler):
         eng = NutsEngine(self.target(), self.Nchain, self.Niter, self.warm_up_num, self.thin_rate, self.d_max,
                          self.dt, cov_p=self.cov_p, rng=rng, seed=seed, fp_mode=self.fp_mode,
                          chain_offset=self.chain_offset, store_chain=self.store_chain, on_dmax=on_dmax,
-                         device=self.device)
+                         device=self.device,
+                         iters_per_call=(self.iters_per_launch or self.Niter) if self.store_chain
+                         else (self.iters_per_launch or 20))                  # (_run's launch sizes)
         if rng == "replay":
             eng.set_replay(*tape)
         t0 = time.time()
