@@ -502,6 +502,9 @@ struct StreamArgs {
 };
 
 constexpr int kStreamChunk = 8;   // window rows loaded together (memory-level parallelism)
+#ifndef HMC_STREAM_PF
+#define HMC_STREAM_PF 8              // rows in flight per wave in k_stream_prod (rolling prefetch)
+#endif
 
 // Block = 4 chain lanes x 64 dims (lane = dim: coalesced rows).  Each thread walks its chains'
 // new rows once, with the last T samples in a register ring.  Two forms of the lag sums:
@@ -664,7 +667,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T <= 16 ? 3
 // in the same order as the difference-form kernel's PROD path had: bit-identical results.
 template <int T>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T <= 16 ? 3 : 1))) void k_stream_prod(StreamArgs a) {
-  constexpr int PF = 8;
+  constexpr int PF = T < HMC_STREAM_PF ? T : HMC_STREAM_PF;
   static_assert(T % PF == 0, "prefetch slots repeat per chunk");
   __shared__ double red[4][kDimTile];
   const int dl = threadIdx.x & (kDimTile - 1);
