@@ -308,6 +308,7 @@ int64_t hmc_random_workspace_size(const hmc_target* t, int64_t n_chains) {
 int64_t hmc_nuts_workspace_size_ex(int32_t D, int64_t n_chains, int32_t d_max, int32_t iters_per_call,
                                    int32_t philox_momenta) {
   if (D < 1 || n_chains < 0 || d_max < 1 || d_max > 15 || iters_per_call < 1) return 0;
+  if (hmc::nuts_lock_path(D)) return hmc::nuts_lock_ws_doubles(n_chains, D, d_max) * (int64_t)sizeof(double);
   if (!hmc::dense_tiles(D)) return hmc::nuts_big_ws_doubles(n_chains, D, d_max) * (int64_t)sizeof(double);
   return hmc::nuts_ws_doubles(n_chains, D, d_max, philox_momenta ? iters_per_call : 0) * (int64_t)sizeof(double);
 }
@@ -345,6 +346,9 @@ hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_s
   }
   a.traj_q = nullptr;
   a.n_save = 0;
+  if (big && hmc::nuts_lock_path(t->D))   // 128 < D <= 320: lockstep 16-chain blocks (hmc_nuts_lock.hip)
+    return hip_status(hmc::launch_nuts_lock(a, s->fp_mode == HMC_MODE_EXACT, replay, (hipStream_t)stream),
+                      "hmc_nuts_iters(lockstep)");
   if (big) return hip_status(hmc::launch_nuts_big(a, s->fp_mode == HMC_MODE_EXACT, replay, (hipStream_t)stream),
                              "hmc_nuts_iters(large D)");
   return hip_status(hmc::launch_nuts_iters(a, s->fp_mode == HMC_MODE_EXACT, replay, (hipStream_t)stream),

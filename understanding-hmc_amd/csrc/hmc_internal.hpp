@@ -72,6 +72,11 @@ int64_t nuts_ws_doubles(int64_t n, int D, int d_max, int mom_iters);   // mom_it
 hipError_t launch_nuts_iters(const RandArgs& a, bool exact, bool replay, hipStream_t s);
 // NUTS for dense D > 128 (hmc_nuts_big.hip): one wave per chain, tree vectors in the workspace.
 int64_t nuts_big_ws_doubles(int64_t n, int D, int d_max);
+// NUTS for 128 < D <= 320 in lockstep 16-chain blocks (hmc_nuts_lock.hip): one MFMA GEMM per block
+// step gives every chain its gradient
+bool nuts_lock_path(int D);
+int64_t nuts_lock_ws_doubles(int64_t n, int D, int d_max);
+hipError_t launch_nuts_lock(const RandArgs& a, bool exact, bool replay, hipStream_t s);
 hipError_t launch_nuts_big(const RandArgs& a, bool exact, bool replay, hipStream_t s);
 
 Layout choose_layout(int D, int L_low, int L_high);
