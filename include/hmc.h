@@ -249,8 +249,9 @@ hmc_status hmc_variogram(const double* x, int64_t n_chains, int64_t chain_stride
  *   row 3 + tmax sum_j (x_j[n-1] - x_j[0])^2: the variogram of lag n - 1, the last lag the ESS loop
  *                reads (:139-150), whatever tmax (0 for n < 2)
  * over the 2*n_chains split chains j (same strided view as hmc_split_moments), S_d = x[base + d]
- * (the view's first sample: a common shift so that B needs no second pass).  tmax in
- * {8, 16, 32, 48, 64}; longer lags: hmc_variogram.  Deterministic (fixed-order two-stage sums). */
+ * (the view's first sample: a common shift so that B needs no second pass).  1 <= tmax <= 4096:
+ * the window is read once whatever tmax (ramp-skipping lag kernel); more lags later for a subset
+ * of dims: hmc_variogram.  Deterministic (fixed-order two-stage sums). */
 int64_t hmc_convergence_work_size(int64_t n_chains, int32_t D, int32_t tmax);
 hmc_status hmc_convergence_sums(const double* x, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
                                 int64_t base, int32_t n, int32_t D, int32_t tmax, double* work, double* out,

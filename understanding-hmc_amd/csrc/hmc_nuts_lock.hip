@@ -90,6 +90,8 @@ __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom 
   double* const ws = G.slots + ((int64_t)blockIdx.x * kLockW + w) * (int64_t)lock_nvec(d_max) * Dp;
   const __amdgpu_buffer_rsrc_t rws = __builtin_amdgcn_make_buffer_rsrc(ws, 0, lock_nvec(d_max) * Dp * 8, 0x00020000);
   const int lo8 = lane * 8;
+  const __amdgpu_buffer_rsrc_t rpf = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(G.pf), 0, G.F * 512,
+                                                                      0x00020000);
   auto wget = [&](int id, int j) -> double {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rws, lo8 + 512 * j, id * Dp * 8, 0));
   };
@@ -245,39 +247,62 @@ __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom 
     if (!alive) break;                                      // (uniform over the block)
     if (w == 0) ++n_steps;
 
-    // ================= the block's GEMM: fragments [f0, f1) of G = P X, partial tiles to LDS
+    // ================= the block's GEMM: fragments [f0, f1) of G = P X, partial tiles to LDS.
+    // Scalar k-step counter and a running LDS address (no division per MFMA); A fragments through a
+    // buffer descriptor with the fragment's offset in the scalar offset.
     {
       typedef double d4 __attribute__((ext_vector_type(4)));
       d4 acc = {0.0, 0.0, 0.0, 0.0};
       const int ch = lane & 15, kh = lane >> 4;
-      int nt_cur = f0 / KS, seg = seg0;
+      int seg = seg0;
+      int ks = f0 - (f0 / KS) * KS;
+      const int xb = kh * kLockXS + ch;
+      int xa = xb + ks * 4 * kLockXS;
       auto flush = [&]() {
         double* t = sSeg + seg * (16 * kLockXS);
 #pragma unroll
         for (int v = 0; v < 4; ++v) t[(4 * v + kh) * kLockXS + ch] = acc[v];
       };
+      auto frag = [&](int f) {
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rpf, lo8 + f * 512, 0, 0));
+      };
+      // four fragments in flight in a static register ring (unrolled by four). Every load is issued
+      // on every path (past f1: a fragment the wave does not use, or zeros past the buffer), and the
+      // ring is complete at the loop entry (the loop header then merges "nothing outstanding" with
+      // the back edge's four in order), so the waitcnt pass keeps three loads outstanding at each
+      // MFMA; a conditional load, a register rotation or a partly loaded ring at the entry made it
+      // drain them all before the MFMAs
       double af[kLockPF];
 #pragma unroll
-      for (int i = 0; i < kLockPF; ++i) af[i] = f0 + i < f1 ? G.pf[(int64_t)(f0 + i) * 64 + lane] : 0.0;
+      for (int i = 0; i < kLockPF; ++i) af[i] = frag(f0 + i);
+#pragma unroll
+      for (int i = 0; i < kLockPF; ++i) asm volatile("" ::"v"(af[i]));   // in hand at the loop entry, so
+      double xc = sX[xa];                                   // B of the current fragment, read one ahead
       for (int fb = f0; fb < f1; fb += kLockPF) {
 #pragma unroll
         for (int i = 0; i < kLockPF; ++i) {
           const int f = fb + i;
-          if (f < f1) {                                     // uniform
-            const int nt = f / KS, ks = f - nt * KS;
-            if (nt != nt_cur) {
+          const bool in = f < f1;
+          const bool last_k = ks + 1 == KS;
+          const int xan = last_k ? xb : xa + 4 * kLockXS;
+          const double xn = sX[xan];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(in ? af[i] : 0.0, xc, acc, 0, 0, 0);
+          af[i] = frag(f + kLockPF);
+          if (in) {
+            if (last_k) {
               flush();
               acc = d4{0.0, 0.0, 0.0, 0.0};
-              nt_cur = nt;
               ++seg;
+              ks = 0;
+            } else {
+              ++ks;
             }
-            const double x = sX[(4 * ks + kh) * kLockXS + ch];
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], x, acc, 0, 0, 0);
-            af[i] = f + kLockPF < f1 ? G.pf[(int64_t)(f + kLockPF) * 64 + lane] : 0.0;
           }
+          xa = xan;
+          xc = xn;
         }
       }
-      if (f1 > f0) flush();
+      if (ks != 0) flush();                                 // a tile the range ends inside
     }
     __syncthreads();
     if (state == LS_LEAP || state == LS_GRAD) {             // this chain's gradient rows, segments in order
