@@ -39,7 +39,7 @@ constexpr int kNutsWaves = HMC_NUTS_WAVES;
 // iteration in another slot; S_GRAD: a fetched chain waits one wave step for the MFMA gradient at
 // its start point.  (A doubling towards the other end starts from that end's q, p, g, loaded at
 // the previous sub-tree's end for the termination check: no load state.)
-enum : int { S_ITER_START = 0, S_SUB_START = 1, S_READY = 2, S_ITER_END = 3, S_DONE = 4, S_FETCH = 5, S_GRAD = 6,
+enum : int { S_ITER_START = 0, S_READY = 2, S_ITER_END = 3, S_DONE = 4, S_FETCH = 5, S_GRAD = 6,
              S_WAIT = 8 };
 
 // Chain hand-off between slots (any CU, any XCD) inside a launch: the chain's state (q, E_prev, tape
@@ -158,6 +158,17 @@ __device__ __forceinline__ void vstore(const WaveWS& w, int v, int vl, const dou
 #pragma unroll
   for (int m = 0; m < M; m += 2) {
     const u32x2 lo = __builtin_bit_cast(u32x2, x[m]), hi = __builtin_bit_cast(u32x2, x[m + 1]);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo.x, lo.y, hi.x, hi.y}, w.r, vo, v * (4 * M * 8) + ws_elem(m), 0);
+  }
+}
+
+// x * sg (sg = +-1: exact) into vector v + vl
+template <int M>
+__device__ __forceinline__ void vstore_sg(const WaveWS& w, int v, int vl, const double (&x)[M], double sg) {
+  const int vo = w.lane_off + vl * (4 * M * 8);
+#pragma unroll
+  for (int m = 0; m < M; m += 2) {
+    const u32x2 lo = __builtin_bit_cast(u32x2, x[m] * sg), hi = __builtin_bit_cast(u32x2, x[m + 1] * sg);
     __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo.x, lo.y, hi.x, hi.y}, w.r, vo, v * (4 * M * 8) + ws_elem(m), 0);
   }
 }
@@ -367,7 +378,7 @@ void k_nuts_iters(RandArgs a) {
   auto write_row_of = [&](int i) { return i >= a.wu && ((i == a.niter) || ((i - a.wu + 1) % a.thin == 0)); };
 
   while (true) {
-    // ================= transitions (ITER_END -> ITER_START -> SUB_START), converged reductions
+    // ================= transitions (ITER_END -> ITER_START -> first doubling), converged reductions
     {
       const bool at_end = state == S_ITER_END;
 #ifdef HMC_DEBUG_HOOKS
@@ -473,10 +484,8 @@ void k_nuts_iters(RandArgs a) {
           for (int m = 0; m < M; ++m) {
             const double z = (h + 4 * m < a.D) ? row[h + 4 * m] : 0.0;
             p[m] = z;
-            if constexpr (MASS) continue;               // K and the boundaries after the products below
+            if constexpr (MASS) continue;               // K after the products below
             kin += z * (dim_minv<MT, GEN>(a, h + 4 * m) * z);
-            vput<M>(W, V_RIGHT_P, m, z);
-            vput<M>(W, V_LEFT_P, m, -z);
           }
         } else if constexpr (PG) {                     // p loaded with the chain's state (S_WAIT)
 #pragma unroll
@@ -484,8 +493,6 @@ void k_nuts_iters(RandArgs a) {
             const double z0 = p[m], z1 = p[m + 1];
             kin += z0 * (dim_minv<MT, GEN>(a, h + 4 * m) * z0);
             kin += z1 * (dim_minv<MT, GEN>(a, h + 4 * m + 4) * z1);
-            vput2<M>(W, V_RIGHT_P, m, z0, z1);
-            vput2<M>(W, V_LEFT_P, m, -z0, -z1);
           }
         } else {
 #pragma unroll
@@ -504,8 +511,6 @@ void k_nuts_iters(RandArgs a) {
             if constexpr (!MASS) {
               kin += z0 * (dim_minv<MT, GEN>(a, d0) * z0);
               kin += z1 * (dim_minv<MT, GEN>(a, d1) * z1);
-              vput2<M>(W, V_RIGHT_P, m, z0, z1);
-              vput2<M>(W, V_LEFT_P, m, -z0, -z1);
             }
             __builtin_amdgcn_sched_barrier(0);
           }
@@ -530,11 +535,7 @@ void k_nuts_iters(RandArgs a) {
           if (starting) {
             kin = kk;
 #pragma unroll
-            for (int m = 0; m < M; ++m) {
-              p[m] = pc[m];
-              vput<M>(W, V_RIGHT_P, m, pc[m]);
-              vput<M>(W, V_LEFT_P, m, -pc[m]);
-            }
+            for (int m = 0; m < M; ++m) p[m] = pc[m];
           }
         }
       }
@@ -547,21 +548,21 @@ void k_nuts_iters(RandArgs a) {
           if (a.dEc) a.dEc[row] = E_init - Eprev;
         }
         vstore<M>(W, V_OLD_Q, old2, q);                 // live_point_q_old = q (:577)
-        vstore<M>(W, V_LEFT_Q, 0, q);                   // left = (q, -p), right = (q, p) (:581-584)
-        gstore<MT>(W, V_LEFT_G, 0, acc);
-        vstore<M>(W, V_RIGHT_Q, 0, q);
-        gstore<MT>(W, V_RIGHT_G, 0, acc);
         E_max_old = E_init;
         pi_old = 1.0;
         d = 0;
         lterm = rterm = false;
         ndraw = 0;
-        state = S_SUB_START;
-      }
-      if (state == S_SUB_START) {                       // first doubling (:595-626) of an iteration
-        Lsub = 1;                                       // d = 0
-        udir = (int)draw(true);                         // :608
-        if (udir != 0) {                                // both ends are (q, +-p): registers hold them
+        // first doubling (:595-626), d = 0: its direction (:608) first, so that only the end it
+        // does not extend is stored (left = (q, -p), right = (q, p), :581-584); the end it extends
+        // is written at the sub-tree's end, before anything reads it
+        Lsub = 1;
+        udir = (int)draw(true);
+        const int o = udir == 0 ? V_LEFT_Q : V_RIGHT_Q;
+        vstore<M>(W, 0, o, q);
+        vstore_sg<M>(W, 1, o, p, udir == 0 ? -1.0 : 1.0);
+        gstore<MT>(W, 2, o, acc);
+        if (udir != 0) {                                // the doubling runs from (q, -p)
 #pragma unroll
           for (int m = 0; m < M; ++m) p[m] = -p[m];
         }
