@@ -174,8 +174,9 @@ int64_t hmc_random_workspace_size(const hmc_target* t, int64_t n_chains);
  * both boundaries, d_max+1 save slots), replay-tape cursors, the launch's work queue and, for
  * Philox runs with a diagonal cov_p (philox_momenta != 0), the momenta drawn ahead of the tree
  * kernel: n_chains x min(32, iters_per_call) x 16*ceil(D/16) doubles (iters_per_call = the largest
- * iter_end - iter_begin the caller will pass).  0 if unsupported.
- * hmc_nuts_workspace_size(D, n, d_max) = ..._ex(D, n, d_max, 32, 1): enough for any call. */
+ * iter_end - iter_begin the caller will pass).  philox_momenta = 0 (replay tapes, or a full cov_p,
+ * which takes the per-chain kernel at every D > 128) sizes for those runs.  0 if unsupported.
+ * hmc_nuts_workspace_size(D, n, d_max): enough for any call (iters_per_call 32, either kind). */
 int64_t hmc_nuts_workspace_size_ex(int32_t D, int64_t n_chains, int32_t d_max, int32_t iters_per_call,
                                    int32_t philox_momenta);
 int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max);

@@ -102,4 +102,4 @@ def test_random_workspace_size_query(monkeypatch):
     assert L.hmc_random_workspace_size(ctypes.byref(H.Target(3000, H.HMC_TARGET_DIAG, None, None, 0.0)), 1000) == \
         2 * 1000 * 3000 * 8 + 3 * 8192
     assert L.hmc_random_workspace_size(ctypes.byref(H.Target(200, H.HMC_TARGET_DENSE, None, None, 0.0)), 1000) == \
-        4 * 1000 * 200 * 8 + 3 * 8192
+        6 * 1000 * 200 * 8 + 3 * 8192   # p, qi, g, gi + the full-cov_p products kv, u

@@ -31,9 +31,15 @@ def _replay(D, cov, q0, dt, fp_mode, N=3, Niter=10, wu=3, thin=1, L=(3, 9), cov_
     from hmc_amd.target import MVNTarget
     rs = np.random.RandomState(D)
     q_start = q0 + rs.standard_normal((N, D))
-    scale = np.sqrt(np.diag(cov_p)) if cov_p is not None else np.ones(D)
-    p0 = rs.standard_normal((N, D)) * scale
-    P = rs.standard_normal((N, Niter, D)) * scale
+    full = cov_p is not None and np.any(cov_p - np.diag(np.diag(cov_p)))
+    if full:                                      # momenta ~ N(0, cov_p) as the reference draws them
+        C = np.linalg.cholesky(cov_p)
+        p0 = rs.standard_normal((N, D)) @ C.T
+        P = rs.standard_normal((N, Niter, D)) @ C.T
+    else:
+        scale = np.sqrt(np.diag(cov_p)) if cov_p is not None else np.ones(D)
+        p0 = rs.standard_normal((N, D)) * scale
+        P = rs.standard_normal((N, Niter, D)) * scale
     Ls = rs.randint(L[0], L[1], size=(N, Niter)).astype(np.int32)
     lnu = np.log(rs.random_sample((N, Niter)))
     tgt = FastMVN(q0, cov)
@@ -70,6 +76,18 @@ def test_dense_large_D_vs_oracle(D, rho, fp_mode):
 
 
 @pytest.mark.parametrize("fp_mode", ["exact", "fast"])
+@pytest.mark.parametrize("D", [136, 300])
+def test_dense_large_D_full_cov_p_vs_oracle(D, fp_mode):
+    """A full (non-diagonal) cov_p above D = 128 (samplers.py:352-356: p ~ N(0, cov_p),
+    K = p.inv(cov_p).p/2, kick by inv(cov_p).dVdq, :811-839): the large-D path's extra GEMMs
+    (kick = inv_cov_p . g, inv_cov_p p at both energies) vs the oracle on the same draws."""
+    import make_golden_shapes as S
+    eng, ref, Ls = _replay(D, O.mvn_cov(D, 0.7), np.linspace(-0.3, 0.3, D), 0.05, fp_mode, cov_p=S.dense_cov_p(D))
+    _check(eng, ref, Ls)
+    np.testing.assert_allclose(eng.dE_chain.cpu().numpy(), ref["dE_chain"], rtol=1e-8, atol=1e-9)
+
+
+@pytest.mark.parametrize("fp_mode", ["exact", "fast"])
 def test_diagonal_large_D_vs_oracle(fp_mode):
     D = 2050
     rs = np.random.RandomState(1)
@@ -80,18 +98,27 @@ def test_diagonal_large_D_vs_oracle(fp_mode):
     _check(eng, ref, Ls)
 
 
-@pytest.mark.parametrize("D,rho,dense", [(160, 0.8, True), (2100, 0.0, False)])
-def test_large_D_philox_stationary(D, rho, dense):
-    """Chains started in N(0, Sigma) stay there (per-dim variance 1, corr rho); runs repeat."""
+@pytest.mark.parametrize("D,rho,dense,full_p", [(160, 0.8, True, False), (2100, 0.0, False, False),
+                                               (160, 0.8, True, True)])
+def test_large_D_philox_stationary(D, rho, dense, full_p):
+    """Chains started in N(0, Sigma) stay there (per-dim variance 1, corr rho), also with a full
+    cov_p (Philox momenta p = C z); runs repeat.  With a cov_p other than the identity the
+    reference's leapfrog (Q3: kick by inv(cov_p).dVdq, drift by p, samplers.py:831-839) does not
+    conserve p.inv(cov_p).p/2 + V: the map is still a volume-preserving, reversible shear pair, so
+    the law is right, but acceptance is low (0 of 1024 at dt = 0.1 for this cov_p, diagonal or
+    not, against 983 with cov_p = I): that case runs at dt = 0.02."""
     from hmc_amd.samplers import HMC_sampler
     from hmc_amd.target import MVNTarget
+    import make_golden_shapes as S
     cov = O.mvn_cov(D, rho) if dense else np.eye(D)
     N = 2048
     qs = np.random.RandomState(3).standard_normal((N, D)) @ np.linalg.cholesky(cov).T
 
     def run():
-        h = HMC_sampler(D, None, None, Nchain=N, Niter=4, sampler_type="Random", L_low=5, L_high=12, dt=0.1,
-                        warm_up_num=1, target=MVNTarget(np.zeros(D), cov), rng="philox", seed=8, fp_mode="fast")
+        h = HMC_sampler(D, None, None, Nchain=N, Niter=4, sampler_type="Random", L_low=5, L_high=12,
+                        dt=0.02 if full_p else 0.1,
+                        warm_up_num=1, target=MVNTarget(np.zeros(D), cov), rng="philox", seed=8, fp_mode="fast",
+                        cov_p=S.dense_cov_p(D) if full_p else None)
         h.gen_sample(qs, verbose=False)
         return h
     h = run()
@@ -99,5 +126,5 @@ def test_large_D_philox_stationary(D, rho, dense):
     assert np.abs(last.var(axis=0).mean() - 1) < 6 * np.sqrt(2 / (N * D)) + 0.01
     if dense:
         assert abs(np.corrcoef(last[:, 0], last[:, 1])[0, 1] - rho) < 6 * (1 - rho ** 2) / np.sqrt(N) + 0.01
-    assert 0.3 < h.accept_R <= 1.0
+    assert (0.05 if full_p else 0.3) < h.accept_R <= 1.0
     assert np.array_equal(h.q_chain, run().q_chain)

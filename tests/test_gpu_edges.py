@@ -71,17 +71,14 @@ def test_empty_chain_batch():
 
 
 def test_unsupported_shapes_raise():
-    """What the kernels still leave out raises NotImplementedError with no launch: a full cov_p
-    above D = 128 (the large-D Random and NUTS paths take a diagonal mass only), d_max > 15."""
+    """What the kernels still leave out raises NotImplementedError with no launch: d_max > 15
+    (the closed-form save slots' range), and chain-0 trajectory capture above D = 128."""
     from hmc_amd.engine import NutsEngine, RandomEngine
     from hmc_amd.target import MVNTarget
     with pytest.raises(NotImplementedError):
-        NutsEngine(MVNTarget(np.zeros(129), O.mvn_cov(129, 0.5)), 2, 4, 0, 1, 6, 0.1, rng="philox",
-                   cov_p=O.mvn_cov(129, 0.3))
-    with pytest.raises(NotImplementedError):
         NutsEngine(MVNTarget(np.zeros(8), np.eye(8)), 2, 4, 0, 1, 16, 0.1, rng="philox")
     D = 136
-    eng = RandomEngine(MVNTarget(np.zeros(D), O.mvn_cov(D, 0.5)), 2, 4, 0, 1, 5, 20, 0.1, rng="philox",
-                       cov_p=O.mvn_cov(D, 0.3))
+    eng = RandomEngine(MVNTarget(np.zeros(D), O.mvn_cov(D, 0.5)), 2, 4, 0, 1, 5, 20, 0.1, rng="philox", n_save=2)
+    eng.init(np.zeros((2, D)))
     with pytest.raises(NotImplementedError):
-        eng.init(np.zeros((2, D)))
+        eng.run(1, 5)

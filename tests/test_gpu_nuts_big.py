@@ -140,14 +140,59 @@ def test_nuts_large_D_philox_stationary_and_shards():
     assert (a[1][res] + b[1][res] == cnt[res]).all()
 
 
-def test_nuts_large_D_full_cov_p_raises():
-    """A full (non-diagonal) cov_p stays limited to D <= 128 for NUTS: NotImplementedError, no launch."""
+@pytest.mark.parametrize("fp_mode", ["exact", "fast"])
+@pytest.mark.parametrize("D", [136, 330])
+def test_nuts_large_D_full_cov_p_vs_oracle(D, fp_mode):
+    """A full (non-diagonal) cov_p above D = 128 (samplers.py:352-356, :811-839 through
+    gen_sample_NUTS): the per-chain kernel's GEMVs (kick = inv_cov_p . P x, K = p.inv_cov_p.p,
+    V from P x) on replayed draws vs the oracle; plus Philox determinism."""
+    import make_golden_shapes as S
+    from hmc_amd import _lib as H
     from hmc_amd.engine import NutsEngine
     from hmc_amd.target import MVNTarget
-    D = 136
-    with pytest.raises(NotImplementedError):
-        NutsEngine(MVNTarget(np.zeros(D), O.mvn_cov(D, 0.5)), 2, 4, 0, 1, 6, 0.1, rng="philox",
-                   cov_p=O.mvn_cov(D, 0.3))
+    N, Niter, wu, dt, d_max = 3, 4, 1, 0.15, 7
+    rs = np.random.RandomState(90 + D)
+    cov, cov_p = O.mvn_cov(D, 0.6), S.dense_cov_p(D)
+    C = np.linalg.cholesky(cov_p)
+    q_start = rs.standard_normal((N, D)) * 1.2
+    p0 = rs.standard_normal((N, D)) @ C.T
+    P = rs.standard_normal((N, Niter, D)) @ C.T
+    tape = rs.uniform(0.0, 2.0, (N, Niter * 2 * (2 ** d_max + d_max + 2)))
+    tgt = FastMVN(np.zeros(D), cov)
+    ref = O.gen_sample_nuts(O.HMCCore(tgt, dt, cov_p), q_start, N, Niter, wu, 1, d_max,
+                            O.ReplayDraws(p0, P, tape=tape.copy()), on_dmax="break")
+    eng = NutsEngine(MVNTarget(np.zeros(D), cov, logdet_const=tgt.c), N, Niter, wu, 1, d_max, dt, cov_p=cov_p,
+                     rng="replay", fp_mode=fp_mode, on_dmax="break")
+    eng.set_replay(p0, P, tape)
+    eng.init(q_start)
+    eng.run(1, Niter + 1)
+    torch.cuda.synchronize()
+    c = eng.read_counters()
+    assert int(c[H.CNT_LEAPFROG]) == ref["n_leapfrog"]
+    assert int(c[H.CNT_UNSTABLE]) == ref["n_unstable"]
+    np.testing.assert_allclose(eng.q_chain.cpu().numpy(), ref["q_chain"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(eng.E_chain.cpu().numpy(), ref["E_chain"], rtol=1e-10, atol=1e-10)
+    if D != 136 or fp_mode != "fast":
+        return
+    # Philox (p = C z): finite and repeatable.  No stationarity check here: the reference's NUTS
+    # with a cov_p other than the identity (Q3 leapfrog, Q11 ratio) does not keep N(0, Sigma) --
+    # the oracle itself, on np.random draws at D = 8, 1,500 chains, 3 iterations, dt = 0.2: mean
+    # per-dim variance 1.38 (full cov_p), 1.30 (its diagonal), 1.05 (identity) -- and the replay
+    # parity above pins this kernel to the reference's behaviour instead.
+    N2 = 256
+    qs = np.random.RandomState(4).standard_normal((N2, D)) @ np.linalg.cholesky(cov).T
+
+    def run():
+        e = NutsEngine(MVNTarget(np.zeros(D), cov), N2, 3, 1, 1, 8, 0.2, cov_p=cov_p, rng="philox", seed=6,
+                       on_dmax="break")
+        e.init(qs)
+        e.run(1, 4)
+        torch.cuda.synchronize()
+        return e.q_chain.cpu().numpy()
+    qc = run()
+    assert np.isfinite(qc).all()
+    assert not np.array_equal(qc[:, -1, :], qc[:, 0, :])
+    assert np.array_equal(qc, run())
 
 
 def test_nuts_large_D_streaming_and_resume(tmp_path):

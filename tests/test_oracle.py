@@ -179,3 +179,24 @@ def test_nuts_closed_form_save_slots():
                 else:
                     for l in check_points(m):
                         assert held.get(slot(int(l), d_max)) == int(l), (d_max, d, m, l)
+
+
+def test_reference_nuts_drifts_with_a_mass_matrix():
+    """A property of the reference the large-D NUTS tests rely on: with cov_p other than the
+    identity, the reference's NUTS (Q3 leapfrog: kick by inv(cov_p).dVdq, drift by p; Q11 ratio;
+    samplers.py:495-808, :831-839) does not keep N(0, Sigma), so GPU runs with a full cov_p are
+    pinned by replay parity, not by a stationarity check.  Oracle on np.random draws, D = 8."""
+    import make_golden_shapes as S
+    np.random.seed(1)
+    D, N = 8, 600
+    cov = O.mvn_cov(D, 0.6)
+    qs = np.random.standard_normal((N, D)) @ np.linalg.cholesky(cov).T
+    var = {}
+    for name, cp in (("full", S.dense_cov_p(D)), ("none", np.eye(D))):
+        np.random.seed(2)
+        ref = O.gen_sample_nuts(O.HMCCore(O.MVNTarget(np.zeros(D), cov), 0.2, cp), qs, N, 3, 1, 1, 8,
+                                O.LiveDraws(D, cp), on_dmax="break")
+        var[name] = ref["q_chain"][:, -1, :].var(axis=0).mean()
+    noise = 6 * np.sqrt(2 / (N * D))
+    assert var["full"] > 1 + noise + 0.1
+    assert abs(var["none"] - 1) < noise + 0.05

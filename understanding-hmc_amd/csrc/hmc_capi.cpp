@@ -186,7 +186,6 @@ hmc_status hmc_chain_init(const hmc_target* t, const hmc_kinetic* k, const hmc_s
   if (s->n_chains == 0) return HMC_OK;
   const bool dense = t->kind == HMC_TARGET_DENSE;
   if (hmc::big_path(dense, t->D)) {   // large D: chain state in the workspace (hmc_big.hip)
-    if (k->minv_full) return fail(HMC_ENOTSUP, "full cov_p with D=%d: not supported", t->D);
     if (!st->order) return fail(HMC_EINVAL, "D=%d needs hmc_random_workspace_size() bytes in state.order", t->D);
     const hmc::Layout lay{0, 0, 0, (t->D + 1) / 2};
     hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
@@ -232,7 +231,6 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
     return fail(HMC_EINVAL, "traj_stride must be >= L_high");
   const bool dense = t->kind == HMC_TARGET_DENSE;
   if (hmc::big_path(dense, t->D)) {   // large D (hmc_big.hip)
-    if (k->minv_full) return fail(HMC_ENOTSUP, "full cov_p with D=%d: not supported", t->D);
     if (st->n_save > 0 && st->traj_q) return fail(HMC_ENOTSUP, "trajectory capture with D=%d: not supported", t->D);
     if (!st->order) return fail(HMC_EINVAL, "D=%d needs hmc_random_workspace_size() bytes in state.order", t->D);
     const hmc::Layout lay{0, 0, 0, (t->D + 1) / 2};
@@ -308,13 +306,18 @@ int64_t hmc_random_workspace_size(const hmc_target* t, int64_t n_chains) {
 int64_t hmc_nuts_workspace_size_ex(int32_t D, int64_t n_chains, int32_t d_max, int32_t iters_per_call,
                                    int32_t philox_momenta) {
   if (D < 1 || n_chains < 0 || d_max < 1 || d_max > 15 || iters_per_call < 1) return 0;
-  if (hmc::nuts_lock_path(D)) return hmc::nuts_lock_ws_doubles(n_chains, D, d_max) * (int64_t)sizeof(double);
+  if (hmc::nuts_lock_path(D)) {   // a full cov_p (philox_momenta 0) takes the per-chain kernel at any D > 128
+    const int64_t lock = hmc::nuts_lock_ws_doubles(n_chains, D, d_max);
+    return (philox_momenta ? lock : std::max(lock, hmc::nuts_big_ws_doubles(n_chains, D, d_max))) *
+           (int64_t)sizeof(double);
+  }
   if (!hmc::dense_tiles(D)) return hmc::nuts_big_ws_doubles(n_chains, D, d_max) * (int64_t)sizeof(double);
   return hmc::nuts_ws_doubles(n_chains, D, d_max, philox_momenta ? iters_per_call : 0) * (int64_t)sizeof(double);
 }
 
 int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max) {
-  return hmc_nuts_workspace_size_ex(D, n_chains, d_max, 32, 1);
+  return std::max(hmc_nuts_workspace_size_ex(D, n_chains, d_max, 32, 1),
+                  hmc_nuts_workspace_size_ex(D, n_chains, d_max, 32, 0));
 }
 
 hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, const hmc_replay* r,
@@ -330,7 +333,6 @@ hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_s
   if (hmc_status e = check_mass(t, k, s)) return e;
   if (t->kind != HMC_TARGET_DENSE) return fail(HMC_ENOTSUP, "NUTS runs the dense kernel: pass prec as dense");
   const bool big = !hmc::dense_tiles(t->D);   // D > 128: hmc_nuts_big.hip
-  if (big && k->minv_full) return fail(HMC_ENOTSUP, "NUTS with a full cov_p and D=%d: not supported", t->D);
   const bool replay = s->rng_mode == HMC_RNG_REPLAY;
   if (replay && (!r || !r->p || !r->tape || r->tape_stride < 1)) return fail(HMC_EINVAL, "replay mode needs p and tape");
   if (s->n_chains == 0 || s->iter_end == s->iter_begin) return HMC_OK;
@@ -346,7 +348,7 @@ hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_s
   }
   a.traj_q = nullptr;
   a.n_save = 0;
-  if (big && hmc::nuts_lock_path(t->D))   // 128 < D <= 320: lockstep 16-chain blocks (hmc_nuts_lock.hip)
+  if (big && hmc::nuts_lock_path(t->D) && !k->minv_full)   // 128 < D <= 320: lockstep 16-chain blocks
     return hip_status(hmc::launch_nuts_lock(a, s->fp_mode == HMC_MODE_EXACT, replay, (hipStream_t)stream),
                       "hmc_nuts_iters(lockstep)");
   if (big) return hip_status(hmc::launch_nuts_big(a, s->fp_mode == HMC_MODE_EXACT, replay, (hipStream_t)stream),

@@ -104,6 +104,9 @@ struct BigArgs {
   double* g;     // [n][D] gradient at q (dense targets)
   double* qi;    // [n][D] q at the start of the iteration (restored on rejection)
   double* gi;    // [n][D] its gradient (dense targets)
+  double* kv;    // [n][D] full cov_p: the kick inv_cov_p g
+  double* u;     // [n][D] full cov_p: inv_cov_p p, or the momentum's z
+  const double* gk;   // the kick vector the leapfrog reads: g, or kv with a full cov_p
   int32_t* L;    // [n] trajectory length of the current iteration
   double* lnu;   // [n] log u of the current iteration
   double* E0;    // [n] energy at the start of the current iteration

@@ -19,6 +19,12 @@
 // an iteration is block kDrawSlot + n (direction = bit 0 of x, uniform = u53(z, w)).
 // This is a shape-range path (the c5 workload is D = 100, hmc_nuts.hip): per leapfrog it reads P
 // once per chain from L2 (D^2 * 8 bytes) instead of sharing it across a 16-chain MFMA tile.
+// 128 < D <= 320 with a diagonal cov_p runs the lockstep kernel (hmc_nuts_lock.hip) instead.
+//
+// A full cov_p (MASS, samplers.py:352-356, :811-839) takes the reference's products as written:
+// p = C z (Philox; replay momenta are the reference's own N(0, cov_p) draws), the kick
+// inv_cov_p . (P x) as two GEMVs, K = p . (inv_cov_p p) with a third, and V from the P x product.
+// The triples then hold the kick vector in their g slot; P x lives in a per-chain scratch vector.
 #include "hmc_device.hpp"
 #include "hmc_internal.hpp"
 
@@ -27,8 +33,10 @@ namespace hmc {
 namespace {
 
 // per-chain vector ids: three (q, p, g) triples (current point, left end, right end), two live
-// points (old / new, :577 / :617), then the d_max + 1 save slots' q and p (:623-626, :654-658)
+// points (old / new, :577 / :617), the d_max + 1 save slots' q and p (:623-626, :654-658), then
+// two scratch vectors of the full-cov_p products (P x of the newest point; inv_cov_p p or z)
 constexpr int kTriples = 3, kLive0 = 3 * kTriples, kSave0 = kLive0 + 2;
+__host__ __device__ constexpr int scratch0(int d_max) { return kSave0 + 2 * (d_max + 1); }
 
 __device__ __forceinline__ double q0_of(const RandArgs& a, int d) { return a.q0 ? a.q0[d] : 0.0; }
 __device__ __forceinline__ double minv_of(const RandArgs& a, int d) { return a.minv ? a.minv[d] : 1.0; }
@@ -41,18 +49,19 @@ struct ChainVecs {
   __device__ double* v(int id) const { return base + (int64_t)id * Dp; }
 };
 
-// g = P (q - q0) for one chain, P row-major symmetric [D][D] (samplers.py:835-837 dVdq)
-__device__ void wave_grad(const RandArgs& a, const double* __restrict__ q, double* __restrict__ g, int lane) {
-  const int D = a.D;
+// y = M (x - shift) for one chain, M row-major [D][D] read as M[k][row]: symmetric matrices
+// (P, inv_cov_p) or a pre-transposed one (cholt = C^T gives C[row][k])
+__device__ void wave_gemv(int D, const double* __restrict__ M, const double* __restrict__ x,
+                          const double* __restrict__ shift, double* __restrict__ y, int lane) {
   for (int r0 = 0; r0 < D; r0 += kWave) {
     const int row = r0 + lane;
     const int rc = row < D ? row : D - 1;
     double acc = 0.0;
     for (int k0 = 0; k0 < D; k0 += kWave) {
       const int kk = k0 + lane;
-      const double xv = kk < D ? q[kk] - q0_of(a, kk) : 0.0;
+      const double xv = kk < D ? x[kk] - (shift ? shift[kk] : 0.0) : 0.0;
       const int kn = min(kWave, D - k0);
-      const double* pk = a.prec + (int64_t)k0 * D + rc;
+      const double* pk = M + (int64_t)k0 * D + rc;
       int j = 0;
       for (; j + 4 <= kn; j += 4) {
         const double p0 = pk[(int64_t)j * D], p1 = pk[(int64_t)(j + 1) * D];
@@ -64,35 +73,52 @@ __device__ void wave_grad(const RandArgs& a, const double* __restrict__ q, doubl
       }
       for (; j < kn; ++j) acc = __builtin_fma(pk[(int64_t)j * D], readlane_d(xv, j), acc);
     }
-    if (row < D) g[row] = acc;
+    if (row < D) y[row] = acc;
   }
 }
 
-// E = V + K = 0.5 (logc + (q - q0).g + p.(minv p))  (samplers.py:811-823)
-__device__ double wave_energy(const RandArgs& a, const double* q, const double* p, const double* g, int lane) {
+// the kick vector at q into g: P (q - q0) (samplers.py:835-837 dVdq), and with a full cov_p
+// inv_cov_p . (P x) with P x kept in gs
+template <bool MASS>
+__device__ void wave_grad(const RandArgs& a, const double* __restrict__ q, double* __restrict__ g,
+                          double* __restrict__ gs, int lane) {
+  if constexpr (MASS) {
+    wave_gemv(a.D, a.prec, q, a.q0, gs, lane);
+    wave_gemv(a.D, a.minvf, gs, nullptr, g, lane);
+  } else {
+    wave_gemv(a.D, a.prec, q, a.q0, g, lane);
+  }
+}
+
+// E = V + K = 0.5 (logc + (q - q0).P x + p.(minv p))  (samplers.py:811-823); P x is g (gs with a
+// full cov_p, whose K takes the product inv_cov_p p into us)
+template <bool MASS>
+__device__ double wave_energy(const RandArgs& a, const double* q, const double* p, const double* g,
+                              const double* gs, double* us, int lane) {
   double maha = 0.0, kin = 0.0;
+  if constexpr (MASS) wave_gemv(a.D, a.minvf, p, nullptr, us, lane);
   for (int d = lane; d < a.D; d += kWave) {
-    maha += (q[d] - q0_of(a, d)) * g[d];
-    kin += p[d] * (minv_of(a, d) * p[d]);
+    maha += (q[d] - q0_of(a, d)) * (MASS ? gs[d] : g[d]);
+    kin += MASS ? p[d] * us[d] : p[d] * (minv_of(a, d) * p[d]);
   }
   return 0.5 * (a.logc + (wave_sum_dpp(maha) + wave_sum_dpp(kin)));
 }
 
 // one leapfrog step (samplers.py:831-839) from (sq, sp, sg) into (q, p, g); may run in place
-template <bool EXACT>
+template <bool EXACT, bool MASS>
 __device__ void wave_leapfrog(const RandArgs& a, const double* sq, const double* sp, const double* sg, double* q,
-                              double* p, double* g, int lane) {
+                              double* p, double* g, double* gs, int lane) {
   for (int d = lane; d < a.D; d += kWave) {
-    const double dt = dt_of(a, d), mi = minv_of(a, d);
+    const double dt = dt_of(a, d), mi = MASS ? 1.0 : minv_of(a, d);
     double pd = sp[d];
     pd = EXACT ? pd - (dt * (mi * sg[d])) * 0.5 : __builtin_fma(-0.5 * dt * mi, sg[d], pd);
     const double qd = EXACT ? sq[d] + dt * pd : __builtin_fma(dt, pd, sq[d]);
     p[d] = pd;
     q[d] = qd;
   }
-  wave_grad(a, q, g, lane);
+  wave_grad<MASS>(a, q, g, gs, lane);
   for (int d = lane; d < a.D; d += kWave) {
-    const double dt = dt_of(a, d), mi = minv_of(a, d);
+    const double dt = dt_of(a, d), mi = MASS ? 1.0 : minv_of(a, d);
     const double pd = p[d];
     p[d] = EXACT ? pd - (dt * (mi * g[d])) * 0.5 : __builtin_fma(-0.5 * dt * mi, g[d], pd);
   }
@@ -137,7 +163,7 @@ __device__ __forceinline__ bool release_fast(int m, int l) {
   return m >= 4 && l > 1;
 }
 
-template <bool EXACT, bool REPLAY>
+template <bool EXACT, bool REPLAY, bool MASS>
 __global__ __launch_bounds__(256) void k_nuts_big(RandArgs a, int Dp, int nv) {
   __shared__ double tab[REPLAY ? 2 : kNormalTableDoubles];
   if constexpr (!REPLAY) {
@@ -150,6 +176,8 @@ __global__ __launch_bounds__(256) void k_nuts_big(RandArgs a, int Dp, int nv) {
   const uint64_t gc = (uint64_t)(a.chain_offset + c);
   const int D = a.D, d_max = a.d_max;
   const ChainVecs W{a.ws + c * (int64_t)nv * Dp, Dp};
+  double* gs = W.v(scratch0(a.d_max));       // P x of the newest point (full cov_p)
+  double* us = W.v(scratch0(a.d_max) + 1);   // inv_cov_p p, or the momentum's z (full cov_p)
   int64_t* tcur = reinterpret_cast<int64_t*>(a.ws + a.n * (int64_t)nv * Dp);
   int64_t tpos = REPLAY ? tcur[c] : 0;
   double* qs = a.q + c * (int64_t)D;
@@ -190,14 +218,22 @@ __global__ __launch_bounds__(256) void k_nuts_big(RandArgs a, int Dp, int nv) {
       }
       const double qd = qs[d];
       tq(rgt)[d] = qd;
-      tp(rgt)[d] = pd;
+      if (MASS && !REPLAY) {
+        us[d] = pd;                                                            // z; p = C z below
+      } else {
+        tp(rgt)[d] = pd;
+        tp(lft)[d] = -pd;
+      }
       tq(lft)[d] = qd;
-      tp(lft)[d] = -pd;
       W.v(old)[d] = qd;
     }
-    wave_grad(a, tq(rgt), tg(rgt), lane);
+    if constexpr (MASS && !REPLAY) {                                           // p ~ N(0, cov_p) (:829)
+      wave_gemv(D, a.cholt, us, nullptr, tp(rgt), lane);
+      for (int d = lane; d < D; d += kWave) tp(lft)[d] = -tp(rgt)[d];
+    }
+    wave_grad<MASS>(a, tq(rgt), tg(rgt), gs, lane);
     wave_copy(D, tg(rgt), tg(lft), lane);
-    const double E_init = wave_energy(a, tq(rgt), tp(rgt), tg(rgt), lane);   // :569
+    const double E_init = wave_energy<MASS>(a, tq(rgt), tp(rgt), tg(rgt), gs, us, lane);   // :569
     if (write_row_of(it) && lane == 0) {                                       // :571-573
       const int64_t row = c * (int64_t)a.Lc + (it - a.wu) / a.thin;
       if (a.Ec) a.Ec[row] = E_init;
@@ -235,17 +271,17 @@ __global__ __launch_bounds__(256) void k_nuts_big(RandArgs a, int Dp, int nv) {
       const int L_new = 1 << d;
       const int udir = (int)draw(true);                                        // :608
       const int from = udir == 0 ? rgt : lft;
-      wave_leapfrog<EXACT>(a, tq(from), tp(from), tg(from), tq(cur), tp(cur), tg(cur), lane);   // :611-614
+      wave_leapfrog<EXACT, MASS>(a, tq(from), tp(from), tg(from), tq(cur), tp(cur), tg(cur), gs, lane);   // :611-614
       ++n_lf;
       wave_copy(D, tq(cur), W.v(nw), lane);                                    // live_q_new (:617)
-      double E_max_now = wave_energy(a, tq(cur), tp(cur), tg(cur), lane);      // :618
+      double E_max_now = wave_energy<MASS>(a, tq(cur), tp(cur), tg(cur), gs, us, lane);   // :618
       double pi_new = 1.0;
       save(1);
       bool reject = false;
       for (int k = 1; k < L_new; ++k) {                                        // :637
-        wave_leapfrog<EXACT>(a, tq(cur), tp(cur), tg(cur), tq(cur), tp(cur), tg(cur), lane);
+        wave_leapfrog<EXACT, MASS>(a, tq(cur), tp(cur), tg(cur), tq(cur), tp(cur), tg(cur), gs, lane);
         ++n_lf;
-        const double E_tmp = wave_energy(a, tq(cur), tp(cur), tg(cur), lane);   // :643
+        const double E_tmp = wave_energy<MASS>(a, tq(cur), tp(cur), tg(cur), gs, us, lane);   // :643
         if (fabs(E_tmp - E_init) > 1000.0) {                                   // :647-651
           reject = true;
           ++n_unst;
@@ -339,7 +375,7 @@ __global__ __launch_bounds__(256) void k_nuts_big(RandArgs a, int Dp, int nv) {
   }
 }
 
-int nuts_big_vectors(int d_max) { return kSave0 + 2 * (d_max + 1); }
+int nuts_big_vectors(int d_max) { return scratch0(d_max) + 2; }
 int nuts_big_padded(int D) { return (D + kWave - 1) / kWave * kWave; }
 
 }  // namespace
@@ -351,12 +387,20 @@ int64_t nuts_big_ws_doubles(int64_t n, int D, int d_max) {
 hipError_t launch_nuts_big(const RandArgs& a, bool exact, bool replay, hipStream_t s) {
   const int Dp = nuts_big_padded(a.D), nv = nuts_big_vectors(a.d_max);
   const dim3 grid((unsigned)((a.n + 3) / 4));
-  if (exact) {
-    if (replay) k_nuts_big<true, true><<<grid, 256, 0, s>>>(a, Dp, nv);
-    else k_nuts_big<true, false><<<grid, 256, 0, s>>>(a, Dp, nv);
+  if (a.minvf) {
+    if (exact) {
+      if (replay) k_nuts_big<true, true, true><<<grid, 256, 0, s>>>(a, Dp, nv);
+      else k_nuts_big<true, false, true><<<grid, 256, 0, s>>>(a, Dp, nv);
+    } else {
+      if (replay) k_nuts_big<false, true, true><<<grid, 256, 0, s>>>(a, Dp, nv);
+      else k_nuts_big<false, false, true><<<grid, 256, 0, s>>>(a, Dp, nv);
+    }
+  } else if (exact) {
+    if (replay) k_nuts_big<true, true, false><<<grid, 256, 0, s>>>(a, Dp, nv);
+    else k_nuts_big<true, false, false><<<grid, 256, 0, s>>>(a, Dp, nv);
   } else {
-    if (replay) k_nuts_big<false, true><<<grid, 256, 0, s>>>(a, Dp, nv);
-    else k_nuts_big<false, false><<<grid, 256, 0, s>>>(a, Dp, nv);
+    if (replay) k_nuts_big<false, true, false><<<grid, 256, 0, s>>>(a, Dp, nv);
+    else k_nuts_big<false, false, false><<<grid, 256, 0, s>>>(a, Dp, nv);
   }
   return hipGetLastError();
 }

@@ -269,8 +269,6 @@ class NutsEngine(RandomEngine):
         assert on_dmax in ("raise", "break")
         self.d_max = int(d_max)
         self.on_dmax = 0 if on_dmax == "raise" else 1
-        if self.D > 128 and self._minv_full is not None:
-            raise NotImplementedError("NUTS with a full cov_p: D=%d not supported (D <= 128)" % self.D)
         # the Philox momenta drawn ahead are sized for the longest run() call (at most 32 iterations
         # are drawn per launch); replay tapes and a full cov_p draw in the kernel and need none
         self.iters_per_call = int(iters_per_call or n_iter)
