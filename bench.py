@@ -91,7 +91,7 @@ def parse(argv=None):
                          "(config 4: D=1000)")
     ap.add_argument("--tmax", type=int, default=16, help="streaming variogram lags")
     ap.add_argument("--stream-feed", type=int, default=0,
-                    help="--stream-diag: steps between diagnostics updates; 0 = auto: every ~120 iterations")
+                    help="--stream-diag: steps between diagnostics updates; 0 = auto: every ~200 iterations")
     ap.add_argument("--no-order-tiles", action="store_true",
                     help="dense targets: MFMA tiles in chain order instead of L-ordered tiles")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -372,10 +372,11 @@ def main():
     offset, N = shard(chains_total, world, rank)
     S = a.iters_per_step if a.iters_per_step > 0 else (16 if nuts else (20 if a.stream_diag else 40))
     W, K = a.warmup, a.steps
-    # streaming diagnostics fed every ~120 iterations: each feed re-reads the last tmax rows (the
-    # variogram carry), so longer feeds cut the bytes per sample from (60+16+12)/60 to (120+16+12)/120
-    # row reads, for a window of tmax + 120 + S + 2 rows (166 GB at c4's 131,072 x D=1000 per GPU)
-    feed_steps = a.stream_feed if a.stream_feed > 0 else max(1, 120 // S)
+    # streaming diagnostics fed every ~200 iterations: each feed re-reads the last tmax rows (the
+    # variogram carry), so longer feeds cut the bytes per sample from (60+16+12)/60 to (200+16+12)/200
+    # row reads, for a window of tmax + 200 + S + 2 rows (250 GB at c4's 131,072 x D=1000 per GPU;
+    # profiles/r04_c4_feed_sweep.txt: feeds of 120 / 180 / 200 iterations 2.24e9 / 2.30e9 / 2.33e9)
+    feed_steps = a.stream_feed if a.stream_feed > 0 else max(1, 200 // S)
     n_iter = (W + K) * S
     wu = W * S + 1                     # chain rows 0 .. K*S-1 are exactly the timed iterations
     timed_rows = K * S
