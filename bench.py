@@ -72,7 +72,7 @@ def parse(argv=None):
     ap.add_argument("--dim", type=int, default=100)
     ap.add_argument("--iters-per-step", type=int, default=0,
                     help="HMC iterations fused into one launch (= one timed step); 0 = auto: 40 for the Random "
-                         "sampler (HMC_sampler.gen_sample fuses a whole run into one launch), 16 for NUTS")
+                         "sampler (HMC_sampler.gen_sample fuses a whole run into one launch), 32 for NUTS (the Philox momenta of up to 32 iterations are drawn ahead per launch)")
     ap.add_argument("--chain-budget-gb", type=float, default=100.0,
                     help="HBM for the circular q_chain window of the timed launches (per GPU)")
     ap.add_argument("--fp-mode", default="fast", choices=["fast", "exact"])
@@ -370,7 +370,7 @@ def main():
     D = a.dim
     chains_total, weak = resolve_chains(a, world)
     offset, N = shard(chains_total, world, rank)
-    S = a.iters_per_step if a.iters_per_step > 0 else (16 if nuts else (20 if a.stream_diag else 40))
+    S = a.iters_per_step if a.iters_per_step > 0 else (32 if nuts else (20 if a.stream_diag else 40))
     W, K = a.warmup, a.steps
     # streaming diagnostics fed every ~200 iterations: each feed re-reads the last tmax rows (the
     # variogram carry), so longer feeds cut the bytes per sample from (60+16+12)/60 to (200+16+12)/200

@@ -71,7 +71,9 @@ typedef unsigned u32x2l __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int save_slot_l(int l, int d_max) { return l == 1 ? d_max : __builtin_ctz(l - 1); }
 
-template <bool EXACT, bool REPLAY>
+// J: coordinates per lane (D <= 64 J): instances J = 3 (D <= 192) and kLockJ, so that the
+// per-chain work of a smaller D issues no fully masked slots (and holds fewer registers)
+template <bool EXACT, bool REPLAY, int J>
 __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom G) {
   __shared__ double sX[kLockDmax * kLockXS];                 // x of the 16 chains, [k][chain]
   __shared__ double sSeg[kLockSegMax * 16 * kLockXS];        // partial output tiles, [row][chain]
@@ -82,7 +84,6 @@ __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom 
   const int w = uniform_i(threadIdx.x / kWave);
   const int D = a.D, d_max = a.d_max;
   const int KS = G.KS, F = G.F;
-  constexpr int J = kLockJ;
   const int Dp = 64 * J;
   // every per-lane access goes through a buffer descriptor (scalar base) with the lane offset
   // lane * 8 and a constant 512 j: no 64-bit address per (array, j) kept live (the 128-register
@@ -555,13 +556,18 @@ hipError_t launch_nuts_lock(const RandArgs& a, bool exact, bool replay, hipStrea
                                                                                                   pf);
   if (hipError_t e = hipGetLastError()) return e;
   const dim3 grid((unsigned)blocks);
-  if (exact) {
-    if (replay) k_nuts_lock<true, true><<<grid, 64 * kLockW, 0, s>>>(a, g);
-    else k_nuts_lock<true, false><<<grid, 64 * kLockW, 0, s>>>(a, g);
-  } else {
-    if (replay) k_nuts_lock<false, true><<<grid, 64 * kLockW, 0, s>>>(a, g);
-    else k_nuts_lock<false, false><<<grid, 64 * kLockW, 0, s>>>(a, g);
-  }
+  auto go = [&](auto jc) {
+    constexpr int J = decltype(jc)::value;
+    if (exact) {
+      if (replay) k_nuts_lock<true, true, J><<<grid, 64 * kLockW, 0, s>>>(a, g);
+      else k_nuts_lock<true, false, J><<<grid, 64 * kLockW, 0, s>>>(a, g);
+    } else {
+      if (replay) k_nuts_lock<false, true, J><<<grid, 64 * kLockW, 0, s>>>(a, g);
+      else k_nuts_lock<false, false, J><<<grid, 64 * kLockW, 0, s>>>(a, g);
+    }
+  };
+  if (a.D <= 64 * 3) go(std::integral_constant<int, 3>{});
+  else go(std::integral_constant<int, kLockJ>{});
   return hipGetLastError();
 }
 
