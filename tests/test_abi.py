@@ -103,3 +103,24 @@ def test_random_workspace_size_query(monkeypatch):
         2 * 1000 * 3000 * 8 + 3 * 8192
     assert L.hmc_random_workspace_size(ctypes.byref(H.Target(200, H.HMC_TARGET_DENSE, None, None, 0.0)), 1000) == \
         6 * 1000 * 200 * 8 + 3 * 8192   # p, qi, g, gi + the full-cov_p products kv, u
+
+
+def test_nuts_workspace_size_query(monkeypatch):
+    """hmc_nuts_workspace_size(_ex) (host-only query): the sized form never exceeds the legacy
+    'any call' size; at 128 < D <= 320 a run without Philox momenta (a replay tape, or a full cov_p,
+    which takes the per-chain kernel) gets at least what the per-chain kernel needs; bad arguments
+    size 0."""
+    from hmc_amd import _lib as H
+    monkeypatch.setattr(H, "_lib", None)
+    L = H.lib()
+    for D in (12, 100, 136, 300, 330):
+        for iters in (1, 8, 32):
+            for pm in (0, 1):
+                ex = L.hmc_nuts_workspace_size_ex(D, 1000, 10, iters, pm)
+                assert 0 < ex <= L.hmc_nuts_workspace_size(D, 1000, 10), (D, iters, pm)
+    lock_philox = L.hmc_nuts_workspace_size_ex(200, 1000, 10, 8, 1)
+    other = L.hmc_nuts_workspace_size_ex(200, 1000, 10, 8, 0)
+    per_chain = L.hmc_nuts_workspace_size_ex(330, 1000, 10, 8, 0) * 200 // 330   # same layout, D-scaled
+    assert other >= lock_philox and other >= per_chain * 0.9
+    assert L.hmc_nuts_workspace_size_ex(100, 1000, 16, 8, 1) == 0          # d_max > 15
+    assert L.hmc_nuts_workspace_size_ex(100, 1000, 10, 0, 1) == 0          # iters_per_call < 1
