@@ -152,22 +152,23 @@ __device__ __forceinline__ constexpr int ws_elem(int m) { return (m >> 1) * 64 +
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-template <int M>
+// N (even, <= M): the vector's slots that can hold a dimension (the rest stay zero untouched)
+template <int M, int N = M>
 __device__ __forceinline__ void vstore(const WaveWS& w, int v, int vl, const double (&x)[M]) {
   const int vo = w.lane_off + vl * (4 * M * 8);
 #pragma unroll
-  for (int m = 0; m < M; m += 2) {
+  for (int m = 0; m < N; m += 2) {
     const u32x2 lo = __builtin_bit_cast(u32x2, x[m]), hi = __builtin_bit_cast(u32x2, x[m + 1]);
     __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo.x, lo.y, hi.x, hi.y}, w.r, vo, v * (4 * M * 8) + ws_elem(m), 0);
   }
 }
 
 // x * sg (sg = +-1: exact) into vector v + vl
-template <int M>
+template <int M, int N = M>
 __device__ __forceinline__ void vstore_sg(const WaveWS& w, int v, int vl, const double (&x)[M], double sg) {
   const int vo = w.lane_off + vl * (4 * M * 8);
 #pragma unroll
-  for (int m = 0; m < M; m += 2) {
+  for (int m = 0; m < N; m += 2) {
     const u32x2 lo = __builtin_bit_cast(u32x2, x[m] * sg), hi = __builtin_bit_cast(u32x2, x[m + 1] * sg);
     __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo.x, lo.y, hi.x, hi.y}, w.r, vo, v * (4 * M * 8) + ws_elem(m), 0);
   }
@@ -198,24 +199,24 @@ __device__ __forceinline__ void vget2(const WaveWS& w, int v, int vl, int m, dou
   x1 = __builtin_bit_cast(double, u32x2{r.z, r.w});
 }
 
-template <int M>
+template <int M, int N = M>
 __device__ __forceinline__ void vload(const WaveWS& w, int v, int vl, double (&x)[M]) {
 #pragma unroll
-  for (int m = 0; m < M; m += 2) vget2<M>(w, v, vl, m, x[m], x[m + 1]);
+  for (int m = 0; m < N; m += 2) vget2<M>(w, v, vl, m, x[m], x[m + 1]);
 }
 
-template <int MT>
+template <int MT, int N = 4 * MT>
 __device__ __forceinline__ void gstore(const WaveWS& w, int v, int vl, const d4 (&acc)[MT]) {
   double x[4 * MT];
 #pragma unroll
   for (int m = 0; m < 4 * MT; ++m) x[m] = acc[m >> 2][m & 3];
-  vstore<4 * MT>(w, v, vl, x);
+  vstore<4 * MT, N>(w, v, vl, x);
 }
 
-template <int MT>
+template <int MT, int N = 4 * MT>
 __device__ __forceinline__ void gload(const WaveWS& w, int v, int vl, d4 (&acc)[MT]) {
 #pragma unroll
-  for (int m = 0; m < 4 * MT; m += 2) {
+  for (int m = 0; m < N; m += 2) {
     double x0, x1;
     vget2<4 * MT>(w, v, vl, m, x0, x1);
     acc[m >> 2][m & 3] = x0;
@@ -310,6 +311,10 @@ template <int MT, bool EXACT, bool GEN, bool REPLAY, bool MASS = false, int SHOR
 __global__ __launch_bounds__(64 * kNutsWaves) __attribute__((amdgpu_waves_per_eu(kNutsWaves / 4, kNutsWaves / 4)))
 void k_nuts_iters(RandArgs a) {
   constexpr int M = 4 * MT;
+  // ME: the slots that can hold a dimension.  The instance compiled for D = 16(MT-1)+1 .. +4
+  // (kShortAlways) needs m <= 4(MT-1) (dims h + 4m < D), rounded up to the 16-byte pairs; every
+  // per-slot loop stops there and the slots past it stay zero (D = 100: 26 of 28)
+  constexpr int ME = SHORT == kShortAlways ? 4 * (MT - 1) + 2 : M;
   // PG: Philox momenta drawn ahead by k_nuts_momenta (all but the dense-mass instances, whose
   // p = C z needs the tile's MFMA product and keeps the in-kernel draws and their tables)
   constexpr bool PG = !REPLAY && !MASS;
@@ -386,14 +391,14 @@ void k_nuts_iters(RandArgs a) {
       if (__builtin_amdgcn_ballot_w64(at_end)) ++ph[13];
 #endif
       if (at_end) {                                     // samplers.py:786-791: q = live_point_q_old
-        vload<M>(W, V_OLD_Q, old2, q);                  // its gradient: recomputed by the slot that
+        vload<M, ME>(W, V_OLD_Q, old2, q);                  // its gradient: recomputed by the slot that
                                                         // takes the chain next (S_GRAD), so the live
                                                         // points keep no gradient vector
         const int qrow = (it - a.wu) / a.thin;
         if (write_row_of(it) && a.qc && qrow >= a.q_row0) {
           double* rowp = a.qc + (c * (int64_t)a.Lq + qrow % a.Lq) * a.D;
 #pragma unroll
-          for (int m = 0; m < M; ++m)
+          for (int m = 0; m < ME; ++m)
             if (h + 4 * m < a.D) rowp[h + 4 * m] = q[m];
         }
         Eprev = E_init;
@@ -402,7 +407,7 @@ void k_nuts_iters(RandArgs a) {
       NUTS_SUBPHASE(8);
       if (state == S_FETCH && live) {                   // tree done: write the chain's state through
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
+        for (int m = 0; m < ME; ++m) {
           const int dd = h + 4 * m;
           if (dd < a.D) st_wt_d(a.q + c * a.D + dd, q[m]);
         }
@@ -456,7 +461,7 @@ void k_nuts_iters(RandArgs a) {
         if (ready) {
           live = true;
 #pragma unroll
-          for (int m = 0; m < M; ++m) {
+          for (int m = 0; m < ME; ++m) {
             const int dd = h + 4 * m;
             q[m] = dd < a.D ? ld_wt_d(a.q + c * a.D + dd) : 0.0;
           }
@@ -465,7 +470,7 @@ void k_nuts_iters(RandArgs a) {
           if constexpr (PG) {                           // this iteration's momentum, with the state
             const double* pv = pm + (c * (a.it1 - a.it0) + (it - a.it0)) * (4 * M) + 2 * h;
 #pragma unroll
-            for (int m = 0; m < M; m += 2) {
+            for (int m = 0; m < ME; m += 2) {
               const double2 z = *reinterpret_cast<const double2*>(pv + 4 * m);
               p[m] = z.x;
               p[m + 1] = z.y;
@@ -481,7 +486,7 @@ void k_nuts_iters(RandArgs a) {
         if constexpr (REPLAY) {
           const double* row = a.rp + (c * (int64_t)a.niter + (it - 1)) * a.D;
 #pragma unroll
-          for (int m = 0; m < M; ++m) {
+          for (int m = 0; m < ME; ++m) {
             const double z = (h + 4 * m < a.D) ? row[h + 4 * m] : 0.0;
             p[m] = z;
             if constexpr (MASS) continue;               // K after the products below
@@ -489,14 +494,14 @@ void k_nuts_iters(RandArgs a) {
           }
         } else if constexpr (PG) {                     // p loaded with the chain's state (S_WAIT)
 #pragma unroll
-          for (int m = 0; m < M; m += 2) {
+          for (int m = 0; m < ME; m += 2) {
             const double z0 = p[m], z1 = p[m + 1];
             kin += z0 * (dim_minv<MT, GEN>(a, h + 4 * m) * z0);
             kin += z1 * (dim_minv<MT, GEN>(a, h + 4 * m + 4) * z1);
           }
         } else {
 #pragma unroll
-          for (int m = 0; m < M; m += 2) {
+          for (int m = 0; m < ME; m += 2) {
             double z0, z1;
             normal_pair_tab(draw_block((uint32_t)(h + 4 * m), (uint32_t)it, gc, a.k0, a.k1), s_ntab, z0, z1);
             const int d0 = h + 4 * m, d1 = d0 + 4;
@@ -523,19 +528,19 @@ void k_nuts_iters(RandArgs a) {
           if constexpr (!REPLAY) {                      // p = C z ~ N(0, cov_p) (samplers.py:829)
             matvec_global<MT>(a.cholt, a.D, lane, p, t);
 #pragma unroll
-            for (int m = 0; m < M; ++m) pc[m] = (h + 4 * m < a.D) ? gval<MT>(t, m) : 0.0;
+            for (int m = 0; m < ME; ++m) pc[m] = (h + 4 * m < a.D) ? gval<MT>(t, m) : 0.0;
           } else {
 #pragma unroll
-            for (int m = 0; m < M; ++m) pc[m] = p[m];
+            for (int m = 0; m < ME; ++m) pc[m] = p[m];
           }
           matvec_global<MT>(a.minvf, a.D, lane, pc, t);
           double kk = 0.0;
 #pragma unroll
-          for (int m = 0; m < M; ++m) kk = mac<EXACT>(kk, pc[m], gval<MT>(t, m));
+          for (int m = 0; m < ME; ++m) kk = mac<EXACT>(kk, pc[m], gval<MT>(t, m));
           if (starting) {
             kin = kk;
 #pragma unroll
-            for (int m = 0; m < M; ++m) p[m] = pc[m];
+            for (int m = 0; m < ME; ++m) p[m] = pc[m];
           }
         }
       }
@@ -547,7 +552,7 @@ void k_nuts_iters(RandArgs a) {
           if (a.Ec) a.Ec[row] = E_init;
           if (a.dEc) a.dEc[row] = E_init - Eprev;
         }
-        vstore<M>(W, V_OLD_Q, old2, q);                 // live_point_q_old = q (:577)
+        vstore<M, ME>(W, V_OLD_Q, old2, q);                 // live_point_q_old = q (:577)
         E_max_old = E_init;
         pi_old = 1.0;
         d = 0;
@@ -559,12 +564,12 @@ void k_nuts_iters(RandArgs a) {
         Lsub = 1;
         udir = (int)draw(true);
         const int o = udir == 0 ? V_LEFT_Q : V_RIGHT_Q;
-        vstore<M>(W, 0, o, q);
-        vstore_sg<M>(W, 1, o, p, udir == 0 ? -1.0 : 1.0);
-        gstore<MT>(W, 2, o, acc);
+        vstore<M, ME>(W, 0, o, q);
+        vstore_sg<M, ME>(W, 1, o, p, udir == 0 ? -1.0 : 1.0);
+        gstore<MT, ME>(W, 2, o, acc);
         if (udir != 0) {                                // the doubling runs from (q, -p)
 #pragma unroll
-          for (int m = 0; m < M; ++m) p[m] = -p[m];
+          for (int m = 0; m < ME; ++m) p[m] = -p[m];
         }
         k = 0;
         state = S_READY;
@@ -594,7 +599,7 @@ void k_nuts_iters(RandArgs a) {
     for (int m = 0; m < (DQV ? M : 1); ++m) dq[m] = 0.0;
     if (act) {
 #pragma unroll
-      for (int m = 0; m < M; ++m) {
+      for (int m = 0; m < ME; ++m) {
         const int dd = h + 4 * m;
         const double dt = dim_dt<MT, GEN>(a, dd), mi = dim_minv<MT, GEN>(a, dd);
         const double pk = p[m], qk = q[m];
@@ -616,7 +621,7 @@ void k_nuts_iters(RandArgs a) {
     NUTS_PHASE(2);
     if (act) {
 #pragma unroll
-      for (int m = 0; m < M; ++m) {
+      for (int m = 0; m < ME; ++m) {
         const int dd = h + 4 * m;
         const double dt = dim_dt<MT, GEN>(a, dd), mi = dim_minv<MT, GEN>(a, dd);
         if constexpr (EXACT) {
@@ -632,7 +637,7 @@ void k_nuts_iters(RandArgs a) {
     double mp1 = 0.0, kp1 = 0.0;
     if constexpr (DQV) {
 #pragma unroll
-      for (int m = 0; m < M; ++m) regA = mac<EXACT>(regA, dq[m], p[m]);
+      for (int m = 0; m < ME; ++m) regA = mac<EXACT>(regA, dq[m], p[m]);
     } else if (!dtv) {
       regA *= a.dt;
       regB *= a.dt;
@@ -641,16 +646,16 @@ void k_nuts_iters(RandArgs a) {
       double xv[M];
       d4 t[MT];
 #pragma unroll
-      for (int m = 0; m < M; ++m) xv[m] = a.q0 ? q[m] - a.q0[min(h + 4 * m, a.D - 1)] : q[m];
+      for (int m = 0; m < ME; ++m) xv[m] = a.q0 ? q[m] - a.q0[min(h + 4 * m, a.D - 1)] : q[m];
       matvec_global<MT>(a.prec, a.D, lane, xv, t);
 #pragma unroll
-      for (int m = 0; m < M; ++m) mp1 = mac<EXACT>(mp1, xv[m], gval<MT>(t, m));
+      for (int m = 0; m < ME; ++m) mp1 = mac<EXACT>(mp1, xv[m], gval<MT>(t, m));
       matvec_global<MT>(a.minvf, a.D, lane, p, t);
 #pragma unroll
-      for (int m = 0; m < M; ++m) kp1 = mac<EXACT>(kp1, p[m], gval<MT>(t, m));
+      for (int m = 0; m < ME; ++m) kp1 = mac<EXACT>(kp1, p[m], gval<MT>(t, m));
     } else {
 #pragma unroll
-      for (int m = 0; m < M; ++m) {
+      for (int m = 0; m < ME; ++m) {
         const int dd = h + 4 * m;
         const double mi = dim_minv<MT, GEN>(a, dd);
         mp1 = mac<EXACT>(mp1, (GEN && a.q0) ? q[m] - a.q0[min(dd, a.D - 1)] : q[m], gval<MT>(acc, m));
@@ -673,12 +678,12 @@ void k_nuts_iters(RandArgs a) {
     const int mpt = k + 1;                              // point number within the sub-tree
     const bool first = act && k == 0, later = act && k > 0;
     if (first) {                                        // first point (:617-626)
-      vstore<M>(W, V_OLD_Q, 2 - old2, q);               // live_point_new (the other buffer pair)
+      vstore<M, ME>(W, V_OLD_Q, 2 - old2, q);               // live_point_new (the other buffer pair)
       maha_new = maha_pt;
       E_max_now = E_tmp;
       pi_new = 1.0;
-      vstore<M>(W, V_SLOTS, 2 * a.d_max, q);            // point 1: save_slot(1)
-      vstore<M>(W, V_SLOTS + 1, 2 * a.d_max, p);
+      vstore<M, ME>(W, V_SLOTS, 2 * a.d_max, q);            // point 1: save_slot(1)
+      vstore<M, ME>(W, V_SLOTS + 1, 2 * a.d_max, p);
       k = 1;
       sub_end = Lsub == 1;
     } else if (later) {
@@ -687,8 +692,8 @@ void k_nuts_iters(RandArgs a) {
         if (h == 0) ++n_unst;
       } else if ((mpt & 3) == 1) {                      // odd point: save (:654-658); 3 (mod 4): see dq
         const int s = save_slot(mpt, a.d_max);
-        vstore<M>(W, V_SLOTS, 2 * s, q);
-        vstore<M>(W, V_SLOTS + 1, 2 * s, p);
+        vstore<M, ME>(W, V_SLOTS, 2 * s, q);
+        vstore<M, ME>(W, V_SLOTS + 1, 2 * s, p);
       }
     }
     NUTS_PHASE(4);
@@ -716,15 +721,15 @@ void k_nuts_iters(RandArgs a) {
       double r_dot = 0.0, l_dot = 0.0;
       if (doit) {
         double qcv[M], pcv[M];
-        vload<M>(W, V_SLOTS, 2 * s, qcv);
-        vload<M>(W, V_SLOTS + 1, 2 * s, pcv);
+        vload<M, ME>(W, V_SLOTS, 2 * s, qcv);
+        vload<M, ME>(W, V_SLOTS + 1, 2 * s, pcv);
         // forward: left = (q_check, -p_check), right = (q, p); backward: left = (q, p),
         // right = (q_check, -p_check).  Both directions reduce to A = (q - qc).p and
         // B = (q - qc).p_check (every sign flip is exact): r_dot, l_dot = (A, B) forward, (B, A)
         // backward, term for term the reference's products.
         double A = 0.0, B = 0.0;
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
+        for (int m = 0; m < ME; ++m) {
           const double Dq = q[m] - qcv[m];
           A = mac<EXACT>(A, Dq, p[m]);
           B = mac<EXACT>(B, Dq, pcv[m]);
@@ -754,7 +759,7 @@ void k_nuts_iters(RandArgs a) {
       pi_new = num + (up ? e : 1.0) * pi_new;
       const double r = num / pi_new;
       if (draw(false) < r) {
-        vstore<M>(W, V_OLD_Q, 2 - old2, q);
+        vstore<M, ME>(W, V_OLD_Q, 2 - old2, q);
         maha_new = maha_pt;
       }
       ++k;
@@ -775,12 +780,12 @@ void k_nuts_iters(RandArgs a) {
       const int o = udir == 0 ? V_LEFT_Q : V_RIGHT_Q;   // the other end
       // the other end's loads first: the stores behind them in the in-order vmcnt queue do not
       // delay the wait for the loads (b != o, so the order changes nothing else)
-      vload<M>(W, 0, o, oqv);
-      vload<M>(W, 1, o, opv);
-      gload<MT>(W, 2, o, og);
-      vstore<M>(W, 0, b, q);
-      vstore<M>(W, 1, b, p);
-      gstore<MT>(W, 2, b, acc);
+      vload<M, ME>(W, 0, o, oqv);
+      vload<M, ME>(W, 1, o, opv);
+      gload<MT, ME>(W, 2, o, og);
+      vstore<M, ME>(W, 0, b, q);
+      vstore<M, ME>(W, 1, b, p);
+      gstore<MT, ME>(W, 2, b, acc);
       const double r = exp(-(E_max_now - E_max_old)) * pi_old / pi_new;   // :766 (Q11)
       const double E_max_old_prev = E_max_old;
       E_max_old = fmax(E_max_old_prev, E_max_now);
@@ -794,7 +799,7 @@ void k_nuts_iters(RandArgs a) {
       // backward: the reference's terms up to exact sign flips
       double tA = 0.0, tB = 0.0;
 #pragma unroll
-      for (int m = 0; m < M; ++m) {
+      for (int m = 0; m < ME; ++m) {
         const double Dq = q[m] - oqv[m];
         tA = mac<EXACT>(tA, Dq, p[m]);
         tB = mac<EXACT>(tB, Dq, opv[m]);
@@ -816,7 +821,7 @@ void k_nuts_iters(RandArgs a) {
         if (nd != udir) {                               // the other end, loaded above
           udir = nd;
 #pragma unroll
-          for (int m = 0; m < M; ++m) {
+          for (int m = 0; m < ME; ++m) {
             q[m] = oqv[m];
             p[m] = opv[m];
           }
