@@ -49,6 +49,10 @@ template <int MT, bool EXACT, bool GEN, bool REPLAY, int WAVES, bool MASS = fals
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVES / 4, WAVES / 4)))
 void k_dense_iters(DenseArgs a) {
   constexpr int M = 4 * MT;
+  // ME: the slots that can hold a dimension.  The instance compiled for D = 16(MT-1)+1 .. +4
+  // (kShortAlways) needs m <= 4(MT-1), rounded up to a pair; the per-slot loops stop there and
+  // the slots past it stay zero (D = 100: 26 of 28)
+  constexpr int ME = SHORT == kShortAlways ? 4 * (MT - 1) + 2 : M;
   extern __shared__ double sP[];
   __shared__ double s_ntab[REPLAY ? 2 : kNormalTableDoubles];   // Box–Muller tables (Philox momentum)
   if constexpr (!REPLAY) init_normal_tables(s_ntab);             // synchronised by stage_precision
@@ -81,6 +85,7 @@ void k_dense_iters(DenseArgs a) {
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     q[m] = (live && dim_ok(m)) ? qh[4 * m] : 0.0;
+    p[m] = 0.0;                                          // (slots past ME are never written)
   }
   double Eprev = live ? a.Eprev[c] : 0.0;
   double* const qcb = a.qc ? a.qc + c * (int64_t)a.Lq * a.D : nullptr;
@@ -103,12 +108,12 @@ void k_dense_iters(DenseArgs a) {
     if constexpr (REPLAY) {
       const double* row = a.rp + (c * (int64_t)a.niter + (it - 1)) * a.D + h;
 #pragma unroll
-      for (int m = 0; m < M; ++m) {
+      for (int m = 0; m < ME; ++m) {
         p[m] = (live && dim_ok(m)) ? row[4 * m] : 0.0;
       }
     } else {
 #pragma unroll
-      for (int m = 0; m < M; m += 2) {
+      for (int m = 0; m < ME; m += 2) {
         double z0 = 0.0, z1 = 0.0;
         if (m < mfull || (m == mfull && mrem > 0)) {   // uniform: pairs wholly in the padding are not drawn
           normal_pair_tab(draw_block(opaque_u32((uint32_t)(h + 4 * m)), (uint32_t)it, gc, a.k0, a.k1), s_ntab, z0,
@@ -127,7 +132,7 @@ void k_dense_iters(DenseArgs a) {
         d4 cz[MT];
         matvec_global<MT>(a.cholt, a.D, lane, p, cz);
 #pragma unroll
-        for (int m = 0; m < M; ++m) p[m] = dim_ok(m) ? gval<MT>(cz, m) : 0.0;
+        for (int m = 0; m < ME; ++m) p[m] = dim_ok(m) ? gval<MT>(cz, m) : 0.0;
       }
     }
     // ---- gradient at q and E0 = V(q) + K(p)  (:434)
@@ -135,7 +140,7 @@ void k_dense_iters(DenseArgs a) {
       gradient<MT, GEN, kDenseDB<WAVES>, SHORT>(a, sP, lane, h, q, acc);
       if (gch && live) {              // keep the cache valid for rejections (q stays, so does g)
 #pragma unroll
-        for (int m = 0; m < M; ++m)
+        for (int m = 0; m < ME; ++m)
           if (dim_ok(m)) gch[4 * m] = gval<MT>(acc, m);
       }
     }
@@ -147,18 +152,18 @@ void k_dense_iters(DenseArgs a) {
       if constexpr (MASS) {
         double xv[M];
 #pragma unroll
-        for (int m = 0; m < M; ++m) xv[m] = a.q0 ? q[m] - a.q0[min(h + 4 * m, a.D - 1)] : q[m];
+        for (int m = 0; m < ME; ++m) xv[m] = a.q0 ? q[m] - a.q0[min(h + 4 * m, a.D - 1)] : q[m];
         d4 t[MT];
         matvec_global<MT>(a.prec, a.D, lane, xv, t);
 #pragma unroll
-        for (int m = 0; m < M; ++m) mh += xv[m] * gval<MT>(t, m);
+        for (int m = 0; m < ME; ++m) mh += xv[m] * gval<MT>(t, m);
         matvec_global<MT>(a.minvf, a.D, lane, p, t);
 #pragma unroll
-        for (int m = 0; m < M; ++m) kn += p[m] * gval<MT>(t, m);
+        for (int m = 0; m < ME; ++m) kn += p[m] * gval<MT>(t, m);
         return;
       }
 #pragma unroll
-      for (int m = 0; m < M; ++m) {       // padded dims contribute exact zeros (g = p = 0)
+      for (int m = 0; m < ME; ++m) {       // padded dims contribute exact zeros (g = p = 0)
         const int d = h + 4 * m;
         const double x = (GEN && a.q0) ? q[m] - a.q0[min(d, a.D - 1)] : q[m];
         mh += x * gval<MT>(acc, m);
@@ -208,7 +213,7 @@ void k_dense_iters(DenseArgs a) {
       const bool act = l < L;
       if (act) {
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
+        for (int m = 0; m < ME; ++m) {
           const int d = h + 4 * m;
           const double dt = dim_dt<MT, GEN>(a, d);
           const double mi = dim_minv<MT, GEN>(a, d);
@@ -225,7 +230,7 @@ void k_dense_iters(DenseArgs a) {
       gradient<MT, GEN, kDenseDB<WAVES>, SHORT>(a, sP, lane, h, q, acc);
       if (act) {
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
+        for (int m = 0; m < ME; ++m) {
           const int d = h + 4 * m;
           const double dt = dim_dt<MT, GEN>(a, d);
           const double mi = dim_minv<MT, GEN>(a, d);
@@ -250,7 +255,7 @@ void k_dense_iters(DenseArgs a) {
     const double dE = E1 - E0;
     const bool accept = (dE < 0.0) || (lnu < -dE);
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
+    for (int m = 0; m < ME; ++m) {
       if (live && dim_ok(m)) {
         if (accept) qh[4 * m] = q[m];
         else q[m] = qh[4 * m];
@@ -258,13 +263,13 @@ void k_dense_iters(DenseArgs a) {
     }
     if (gch && live && accept) {      // the gradient at the new q (a rejection keeps the cached one)
 #pragma unroll
-      for (int m = 0; m < M; ++m)
+      for (int m = 0; m < ME; ++m)
         if (dim_ok(m)) gch[4 * m] = gval<MT>(acc, m);
     }
     if (live && write_row && qcb && row >= a.q_row0) {
       double* rowp = qcb + (row % a.Lq) * a.D + h;
 #pragma unroll
-      for (int m = 0; m < M; ++m) {
+      for (int m = 0; m < ME; ++m) {
         if (dim_ok(m)) __builtin_nontemporal_store(q[m], rowp + 4 * m);   // sample row: written once
       }
     }
