@@ -473,7 +473,10 @@ def main():
                    rhat_median=float(np.median(R_hat)), rhat_max=float(np.max(R_hat)),
                    samples_per_chain=n_samples, sampling_s=t_samples, diagnostics_s=diag_s,
                    diagnostics_lags=dict(LAST_INFO),
-                   method=(f"streaming statistics (tmax={a.tmax}) over every timed sample, fed inside the timed loop"
+                   method=(("reference estimator (every lag 1..n-1) over every timed sample: each split half "
+                            "fed to the one-read lag kernel once complete, inside the timed loop"
+                            if sd.mode == "exact" else
+                            f"streaming statistics (tmax={a.tmax}) over every timed sample, fed inside the timed loop")
                            if sd is not None else
                            f"reference estimator on the circular window's last {R} samples per chain (all chains), "
                            f"after the timed loop; ESS/s = n_eff / time of the {R} iterations that produced them "
@@ -484,13 +487,18 @@ def main():
     if rank == 0:
         dense = a.rho != 0 or nuts
         lf_launch = lf_local / K
+        # kernel dispatches per timed step: the dense Random path with L-ordered tiles launches one
+        # tile kernel per iteration (chains counting-sorted by that iteration's L); every other path
+        # fuses the step's S iterations into one dispatch
+        ordered = a.rho != 0 and not nuts and not a.no_order_tiles
+        dispatches = S if ordered else 1
         # SURVEY.md §8(d) algorithmic bytes: 24*D + 24 per chain-iteration (read q, write q, write the
         # sample row, write E and dE) -- the unfused per-iteration contract
         bytes_model = N * S * (24 * D + 24)
-        # what the fused launch must move: per chain-iteration one q_chain row + E + dE; q and E_prev
-        # read and written once per launch
+        # what the step's dispatches must move: per chain-iteration one q_chain row + E + dE; q and
+        # E_prev read and written once per dispatch
         row_bytes = 8 * D if (store or sd is not None) else 0
-        bytes_moved = N * (S * (row_bytes + 16) + 16 * D + 16)
+        bytes_moved = N * (S * (row_bytes + 16) + dispatches * (16 * D + 16))
         if dense:   # 2D^2 + 7D per leapfrog (Random dense), 2D^2 + 12D (NUTS: E + U-turn dots)
             flops_launch = lf_launch * (2 * D * D + (12 if nuts else 7) * D)
         else:       # 8D per leapfrog + 8D energies per iteration
@@ -502,22 +510,29 @@ def main():
         shape = dict(kernel=kname, dim=D, chains_per_gpu=N, iters_per_step=S, window_rows=R,
                      stream_diag=bool(a.stream_diag), rho=a.rho)
         pm = pmc_traffic(shape)
-        traffic = None if pm is None else pm["bytes_per_launch"]
+        # PMC bytes are per hot-kernel DISPATCH (summarize_profile.py averages the timed dispatches);
+        # kernel_ms times the step's dispatches together, so the step's traffic is dispatches x that
+        traffic_dispatch = None if pm is None else pm["bytes_per_launch"]
+        traffic = None if pm is None else traffic_dispatch * dispatches
+        frac_meas = None if pm is None else traffic / kern_s / 1e9 / HBM_PEAK_GBS
         hbm = {"bound": "hbm", "achieved": bytes_model / kern_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": bytes_model / kern_s / 1e9 / HBM_PEAK_GBS,
-               "traffic": traffic,
+               # what the fused dispatches must move (rows + E/dE + q and E_prev in and out per
+               # dispatch) over the same time, next to the §8(d) model's unfused traffic above
+               "frac_required": bytes_moved / kern_s / 1e9 / HBM_PEAK_GBS,
+               "bytes_required_per_step": bytes_moved,
+               "traffic": traffic, "traffic_per_dispatch": traffic_dispatch, "dispatches_per_step": dispatches,
                "traffic_source": None if pm is None else pm.get("source"),
-               # measured HBM bytes (same-shape rocprofv3 PMC run) over the same kernel time: what
-               # the fused kernel actually moves, against the §8(d) model's unfused traffic above
-               "frac_measured": None if pm is None else traffic / kern_s / 1e9 / HBM_PEAK_GBS,
+               # measured HBM bytes (same-shape rocprofv3 PMC run) over the same kernel time
+               "frac_measured": frac_meas,
                "kernel": kname, "kernel_ms": kern_ms, "bytes_per_launch": bytes_model, "shape": shape,
-               "bytes_model": "SURVEY.md §8(d): (24*D + 24) B per chain-iteration x chains x iterations per launch",
-               "bytes_moved_per_launch": bytes_moved,
-               "frac_moved": bytes_moved / kern_s / 1e9 / HBM_PEAK_GBS}
+               "bytes_model": "SURVEY.md §8(d): (24*D + 24) B per chain-iteration x chains x iterations per step"}
         mfma = {"bound": "mfma" if dense else "fp64 vector", "achieved": tfl, "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": tfl / FP64_PEAK_TFLOPS,
-                "traffic": traffic, "shape": shape, "kernel": kname,
-                "hbm_frac_measured": None if pm is None else traffic / kern_s / 1e9 / HBM_PEAK_GBS,
+                "traffic": traffic, "traffic_per_dispatch": traffic_dispatch, "dispatches_per_step": dispatches,
+                "traffic_source": None if pm is None else pm.get("source"),
+                "shape": shape, "kernel": kname,
+                "hbm_frac_measured": frac_meas,
                 "kernel_ms": kern_ms, "flops_per_launch": flops_launch}
         if sd is not None:
             # the timed step also feeds the streaming diagnostics: `frac` above prices the sampler
@@ -547,8 +562,10 @@ def main():
             "dtype": "f64",
             "data": f"synthetic (D={D} {tdesc}, starts ~ N(0, 2I) keyed by global chain id, Philox4x32-10 draws)",
             "config": {"workload": f"{samp}, D={D} {tdesc}, dt={a.dt}, {chains_total} chains in total "
-                                   f"({N} on rank 0), {S} iterations per step (one fused launch), "
-                                   f"{store_desc}, fp_mode={a.fp_mode}",
+                                   f"({N} on rank 0), {S} iterations per step "
+                                   + (f"({S} launches per step: one per iteration, L-ordered tiles)" if ordered
+                                      else "(one fused launch)") +
+                                   f", {store_desc}, fp_mode={a.fp_mode}",
                        "preset": a.config, "chains_total": chains_total, "chains_per_gpu": N, "dim": D,
                        "iters_per_step": S, "window_rows": R, "parallelism": f"chains{world}",
                        "backend": a.backend if world > 1 else None},

@@ -47,7 +47,8 @@ enum {
   HMC_CNT_ACCEPT = 0,        /* accepted proposals, i >= warm_up (samplers.py:467)          */
   HMC_CNT_ACCEPT_WU = 1,     /* accepted proposals, i <  warm_up (samplers.py:469)          */
   HMC_CNT_LEAPFROG = 2,      /* sum of L actually integrated (the metric's unit of work)     */
-  HMC_CNT_LEAPFROG_SQ = 3,   /* Random: sum of L^2 (N_total_steps, Q13); NUTS: wave steps    */
+  HMC_CNT_LEAPFROG_SQ = 3,   /* Random: sum of L^2 (N_total_steps, Q13); NUTS: steps of the
+                                kernel's scheduling unit (see hmc_nuts_iters)                 */
   HMC_CNT_OOB_REJECT = 4,    /* rejections whose warm-up row index is < -L_chain (Q5)        */
   HMC_CNT_UNSTABLE = 5,      /* NUTS |E-E0| > 1000 sub-tree rejections (samplers.py:647)     */
   HMC_CNT_DMAX = 6,          /* NUTS chain-iterations that hit d_max                         */
@@ -80,7 +81,8 @@ typedef struct hmc_kinetic {
   double dt;               /* scalar step                                                 */
   /* Dense (non-diagonal) mass matrix, samplers.py:352-356 with a full cov_p (Q3 semantics:
    * K = p.inv(cov_p).p/2, kick by inv(cov_p).dVdq, drift by p).  All NULL => diagonal/identity
-   * via minv/p_scale above (which must then be NULL).  Random sampler, dense targets only.  */
+   * via minv/p_scale above (which must then be NULL).  Dense targets (pass prec dense), any D,
+   * Random and NUTS samplers (NUTS reads minv_full and kick; p_chol_t for Philox draws).  */
   const double* minv_full; /* [D*D] inv(cov_p), row-major (symmetric)                     */
   const double* p_chol_t;  /* [D*D] transpose of the lower Cholesky factor C of cov_p:
                               Philox momentum p = C z, z ~ N(0, I)                        */
@@ -168,8 +170,12 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
                             const hmc_replay* r /* NULL for Philox */, hmc_state* st, void* stream);
 
 /* Bytes of the optional hmc_state.order scratch for hmc_random_iters on this target
- * (0 for diagonal targets, which need none): the tile order plus the gradient cache. */
+ * (0 for diagonal targets, which need none): the tile order plus the gradient cache.  Large-D
+ * targets (dense D > 128, diagonal D > 2048) keep their chain state there and need it, also for
+ * hmc_chain_init of a NUTS run.  hmc_random_workspace_size covers either cov_p; the _ex form sizes
+ * for the given kinetic part (two [n][D] vectors fewer without a full cov_p). */
 int64_t hmc_random_workspace_size(const hmc_target* t, int64_t n_chains);
+int64_t hmc_random_workspace_size_ex(const hmc_target* t, const hmc_kinetic* k, int64_t n_chains);
 /* Bytes of device workspace hmc_nuts_iters needs for n_chains chains: tree vectors (live points,
  * both boundaries, d_max+1 save slots), replay-tape cursors, the launch's work queue and, for
  * Philox runs with a diagonal cov_p (philox_momenta != 0), the momenta drawn ahead of the tree
@@ -185,15 +191,30 @@ int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max);
  * resample -> E0 -> tree doubling until both ends U-turn (sub-tree U-turn checks against the
  * saved odd points, progressive sampling, biased sub-tree acceptance) -> store.
  * Replaces HMC_sampler.gen_sample_NUTS, samplers.py:563-791 (+ utils.py:222-385).
- * Dense precision only (pass diagonal targets as dense), any D, 1 <= d_max <= 15: D <= 128 runs
- * the 16-chain MFMA tree kernel, D > 128 one wave per chain (diagonal cov_p only there).
- * `workspace` (hmc_nuts_workspace_size bytes) must be zeroed before the first call of a run
- * and kept between calls.  Counters: LEAPFROG (= ENERGY_EVALS), UNSTABLE (|E-E0| > 1000
- * rejections, :647), DMAX (chain-iterations that reached d_max; the reference aborts there,
- * on_dmax selects whether the caller raises), OOB_REJECT (replay tape exhausted: an error). */
+ * Dense precision only (pass diagonal targets as dense), any D, 1 <= d_max <= 15 (the reference
+ * takes any d_max; 15 = 2^15 - 1 leapfrogs per tree, documented in INTEGRATION.md), diagonal or
+ * full cov_p (minv_full) at any D:
+ *   D <= 128              the 16-chain MFMA tree kernel (hmc_nuts.hip; a full cov_p adds its
+ *                         momentum and kinetic products on the same tiles);
+ *   128 < D <= 320        diagonal cov_p: 16 chains per block in lockstep sharing one MFMA GEMM per
+ *                         leapfrog (hmc_nuts_lock.hip);
+ *   otherwise (D > 320, or a full cov_p at any D > 128) one wave per chain (hmc_nuts_big.hip;
+ *                         a full cov_p as three GEMVs per leapfrog).
+ * `workspace` (hmc_nuts_workspace_size bytes, or hmc_nuts_workspace_size_ex sized for the calls
+ * made) must be zeroed before the first call of a run and kept between calls; hmc_nuts_iters_ws
+ * also takes the workspace's size and refuses (HMC_EINVAL) a call that needs more.  Counters:
+ * LEAPFROG (= ENERGY_EVALS), UNSTABLE (|E-E0| > 1000 rejections, :647), DMAX (chain-iterations
+ * that reached d_max; the reference aborts there, on_dmax selects whether the caller raises),
+ * OOB_REJECT (replay tape exhausted: an error), LEAPFROG_SQ = steps of the kernel's scheduling
+ * unit, whose meaning depends on the path: wave steps of the 16-chain tree kernel and block steps
+ * of the lockstep kernel (16 chain slots each: lane utilisation = LEAPFROG / (16 x LEAPFROG_SQ)),
+ * wave steps of the per-chain kernel (one chain per wave: equal to LEAPFROG). */
 hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s,
                           const hmc_replay* r /* NULL for Philox */, hmc_state* st, void* workspace,
                           void* stream);
+hmc_status hmc_nuts_iters_ws(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s,
+                             const hmc_replay* r /* NULL for Philox */, hmc_state* st, void* workspace,
+                             int64_t workspace_bytes, void* stream);
 
 /* Batched single leapfrog step (n independent (p, q) rows).
  * Replaces HMC_sampler.leap_frog(p_old, q_old), samplers.py:831-839. */
@@ -220,7 +241,11 @@ hmc_status hmc_philox(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3, uint32
  * mean/std of plot_samples (samplers.py:213, :246).  Chains are read in place:
  * element (chain m, sample s, dim d) = x[base + m*chain_stride + s*sample_stride + d].
  * All sums are deterministic (fixed-order two-stage reductions); `work` is caller-owned
- * scratch of the size the *_work_size query returns (doubles). */
+ * scratch of the size the *_work_size query returns (doubles).
+ * Lag passes (hmc_variogram, hmc_convergence_sums, hmc_half_sums) address a chain's samples with
+ * 32-bit buffer offsets: one chain's span (about 3 x chain_stride doubles) must stay within 1 GiB,
+ * e.g. D = 1000 up to ~40,000 stored samples per chain; larger views return HMC_ENOTSUP (pass a
+ * contiguous copy of fewer dimensions; hmc_amd.diagnostics does so by itself). */
 
 /* Per split chain j (= 2m + half; half h covers samples [h*n, h*n+n)): mean and std
  * (ddof=1) of every dimension -> mean_out/std_out [2*n_chains][D].  utils.py:88-119. */
@@ -235,7 +260,8 @@ hmc_status hmc_rowsum(const double* x, int64_t n_outer, int64_t outer_stride, in
                       double* out, void* stream);
 
 /* Variogram sums out[t - t0][d] = sum_j sum_s (x_j[s+t] - x_j[s])^2 over split chains,
- * lags t in [t0, t1).  utils.py:161-179 (before its division by m*(n-t)). */
+ * lags t in [t0, t1), 1 <= t1 - t0 <= 2^20 (one read of the samples for any lag count; work grows
+ * with it).  utils.py:161-179 (before its division by m*(n-t)). */
 int64_t hmc_variogram_work_size(int64_t n_chains, int32_t D, int32_t nlags);
 hmc_status hmc_variogram(const double* x, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
                          int64_t base, int32_t n, int32_t D, int32_t t0, int32_t t1, double* work, double* out,
@@ -250,13 +276,25 @@ hmc_status hmc_variogram(const double* x, int64_t n_chains, int64_t chain_stride
  *   row 3 + tmax sum_j (x_j[n-1] - x_j[0])^2: the variogram of lag n - 1, the last lag the ESS loop
  *                reads (:139-150), whatever tmax (0 for n < 2)
  * over the 2*n_chains split chains j (same strided view as hmc_split_moments), S_d = x[base + d]
- * (the view's first sample: a common shift so that B needs no second pass).  1 <= tmax <= 4096:
- * the window is read once whatever tmax (ramp-skipping lag kernel); more lags later for a subset
- * of dims: hmc_variogram.  Deterministic (fixed-order two-stage sums). */
+ * (the view's first sample: a common shift so that B needs no second pass).  1 <= tmax <= 2^20:
+ * the window is read once whatever tmax (ramp-skipping lag kernel); tmax >= n - 2 gives every lag
+ * the ESS loop can read (the last few in difference form); more lags later for a subset of dims:
+ * hmc_variogram.  Deterministic (fixed-order two-stage sums). */
 int64_t hmc_convergence_work_size(int64_t n_chains, int32_t D, int32_t tmax);
 hmc_status hmc_convergence_sums(const double* x, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
                                 int64_t base, int32_t n, int32_t D, int32_t tmax, double* work, double* out,
                                 void* stream);
+
+/* hmc_convergence_sums for ONE completed split half of every chain, read in place from a circular
+ * streaming window: sample s (0 <= s < n) of chain c, dim d at window[c*chain_stride +
+ * ((slot0 + s) % wrap)*sample_stride + d] (wrap 0: row slot0 + s).  Same output layout over the
+ * n_chains series (one per chain) with S_d = chain 0's sample 0; additive over halves and ranks
+ * after re-centring (hmc_amd.diagnostics.StreamingDiagnostics): the streaming run's R-hat and ESS
+ * then use every lag 1 .. n-1, exactly as convergence_stats on the stored q_chain (utils.py:77-179).
+ * work: hmc_convergence_work_size(n_chains, D, tmax) doubles. */
+hmc_status hmc_half_sums(const double* window, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
+                         int32_t D, int32_t wrap, int32_t slot0, int32_t n, int32_t tmax, double* work, double* out,
+                         void* stream);
 
 /* Streaming (windowed) split-chain statistics for runs whose q_chain does not fit: feed the
  * samples segment by segment.  Positions p index q_chain[:, 1:, :] (Q16); p lies in split half

@@ -103,6 +103,14 @@ def test_random_workspace_size_query(monkeypatch):
         2 * 1000 * 3000 * 8 + 3 * 8192
     assert L.hmc_random_workspace_size(ctypes.byref(H.Target(200, H.HMC_TARGET_DENSE, None, None, 0.0)), 1000) == \
         6 * 1000 * 200 * 8 + 3 * 8192   # p, qi, g, gi + the full-cov_p products kv, u
+    # sized for the kinetic part: without a full cov_p no kv, u (advisor r04)
+    diag_k = H.Kinetic(None, None, None, 0.1, None, None, None)
+    full_k = H.Kinetic(None, None, None, 0.1, 1, 1, 1)             # any non-NULL minv_full
+    t200 = ctypes.byref(H.Target(200, H.HMC_TARGET_DENSE, None, None, 0.0))
+    assert L.hmc_random_workspace_size_ex(t200, ctypes.byref(diag_k), 1000) == 4 * 1000 * 200 * 8 + 3 * 8192
+    assert L.hmc_random_workspace_size_ex(t200, ctypes.byref(full_k), 1000) == 6 * 1000 * 200 * 8 + 3 * 8192
+    assert L.hmc_random_workspace_size_ex(ctypes.byref(H.Target(100, H.HMC_TARGET_DENSE, None, None, 0.0)),
+                                          ctypes.byref(diag_k), 1000) == (1000 + 512) * 4 + 16 + 1000 * 100 * 8
 
 
 def test_nuts_workspace_size_query(monkeypatch):
@@ -124,3 +132,23 @@ def test_nuts_workspace_size_query(monkeypatch):
     assert other >= lock_philox and other >= per_chain * 0.9
     assert L.hmc_nuts_workspace_size_ex(100, 1000, 16, 8, 1) == 0          # d_max > 15
     assert L.hmc_nuts_workspace_size_ex(100, 1000, 10, 0, 1) == 0          # iters_per_call < 1
+
+
+def test_nuts_sized_entry_refuses_small_workspace(monkeypatch):
+    """hmc_nuts_iters_ws checks the workspace size on the host before anything runs (advisor r04: a
+    workspace sized for fewer Philox momentum iterations, or none, was a silent device overrun):
+    EINVAL -> AssertionError, no GPU needed."""
+    from hmc_amd import _lib as H
+    monkeypatch.setattr(H, "_lib", None)
+    L = H.lib()
+    D, n, d_max = 100, 1000, 10
+    T = H.Target(D, H.HMC_TARGET_DENSE, None, 1, 0.0)              # prec: any non-NULL pointer (not read)
+    K = H.Kinetic(None, None, None, 0.1, None, None, None)
+    st = H.State(1, 1)                                              # q, E_prev non-NULL (not read)
+    S = H.Schedule(n, 0, 100, 0, 1, 101, 5, 20, 1, 33, H.HMC_RNG_PHILOX, H.HMC_MODE_FAST, d_max, 1, 0)
+    small = L.hmc_nuts_workspace_size_ex(D, n, d_max, 8, 1)        # sized for 8 iterations per call
+    with pytest.raises(AssertionError, match="needs"):
+        H.check(L.hmc_nuts_iters_ws(T, K, S, None, st, 1, small, None), "x")     # a 32-iteration call
+    none = L.hmc_nuts_workspace_size_ex(D, n, d_max, 32, 0)        # sized without Philox momenta
+    with pytest.raises(AssertionError, match="needs"):
+        H.check(L.hmc_nuts_iters_ws(T, K, S, None, st, 1, none, None), "x")

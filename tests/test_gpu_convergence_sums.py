@@ -47,6 +47,12 @@ CASES = [
     (7, 101, 100, 0, 1, 1, 48),        # n = 50 (the bench window), 48 lags: 3-wave blocks
     (4, 201, 130, 0, 1, 1, 48),        # n = 100 > 48
     (6, 101, 101, 0, 1, 1, 48),        # odd D, 48 lags -> register-staged kernel (an idle wave)
+    # complete passes (tmax >= n - 2): lag groups up to n - 1 - tail, the tail in difference form
+    (6, 199, 100, 0, 1, 1, 97),        # n = 99 (c4's halves): two groups of 48 + a tail of 2
+    (3, 401, 100, 0, 1, 1, 198),       # n = 200 (c3's window): four groups + a tail of 7
+    (5, 115, 70, 0, 1, 1, 55),         # n = 57: one group + the longest tail, 8
+    (5, 117, 70, 0, 1, 1, 56),         # n = 58: two groups (a tail of 9 would exceed 8)
+    (4, 240, 100, 0, 1, 1, 150),       # tmax beyond n - 1 = 119: the lags past it are 0
 ]
 
 

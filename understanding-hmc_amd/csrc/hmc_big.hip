@@ -374,11 +374,13 @@ hipError_t mass_momentum(const BigArgs& b, bool replay, hipStream_t s) {
 
 bool big_path(int kind_dense, int D) { return kind_dense ? dense_tiles(D) == 0 : (D + 1) / 2 > 16 * kWave; }
 
-// vectors: p, qi; dense targets also g, gi and the full-cov_p products kv, u
-int64_t big_workspace_bytes(int64_t n, int D, bool dense) {
+// vectors: p, qi; dense targets also g, gi and, with a full cov_p, its products kv, u
+static int big_vectors(bool dense, bool full_mass) { return dense ? (full_mass ? 6 : 4) : 2; }
+
+int64_t big_workspace_bytes(int64_t n, int D, bool dense, bool full_mass) {
   const int64_t v = ((n * (int64_t)D * 8 + 255) / 256) * 256;
   const int64_t s = ((n * 8 + 255) / 256) * 256;
-  return v * (dense ? 6 : 2) + 3 * s;
+  return v * big_vectors(dense, full_mass) + 3 * s;
 }
 
 BigArgs big_args(const RandArgs& a, void* ws, bool dense) {
@@ -392,11 +394,13 @@ BigArgs big_args(const RandArgs& a, void* ws, bool dense) {
   if (dense) {
     b.g = reinterpret_cast<double*>(p + 2 * v);
     b.gi = reinterpret_cast<double*>(p + 3 * v);
-    b.kv = reinterpret_cast<double*>(p + 4 * v);
-    b.u = reinterpret_cast<double*>(p + 5 * v);
+    if (a.minvf) {
+      b.kv = reinterpret_cast<double*>(p + 4 * v);
+      b.u = reinterpret_cast<double*>(p + 5 * v);
+    }
     b.gk = a.minvf ? b.kv : b.g;
   }
-  char* t = p + v * (dense ? 6 : 2);
+  char* t = p + v * big_vectors(dense, a.minvf != nullptr);
   b.L = reinterpret_cast<int32_t*>(t);
   b.lnu = reinterpret_cast<double*>(t + s);
   b.E0 = reinterpret_cast<double*>(t + 2 * s);

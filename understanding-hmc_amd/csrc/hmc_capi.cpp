@@ -155,6 +155,14 @@ bool general_diag(const hmc_target* t, const hmc_kinetic* k) {
   return t->q0 || t->prec || k->minv || k->p_scale || k->dt_vec;
 }
 
+constexpr int32_t kMaxLags = 1 << 20;   // lag passes of the diagnostics (any n the samples allow)
+
+hmc_status view_too_large(const char* what) {
+  return fail(HMC_ENOTSUP,
+              "%s: one chain's samples span more than the lag kernel's 1 GiB buffer offsets; pass fewer "
+              "dimensions per call (the Python layer splits such views by dimension)", what);
+}
+
 }  // namespace
 
 extern "C" {
@@ -295,12 +303,16 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
   return HMC_OK;
 }
 
-int64_t hmc_random_workspace_size(const hmc_target* t, int64_t n_chains) {
+int64_t hmc_random_workspace_size_ex(const hmc_target* t, const hmc_kinetic* k, int64_t n_chains) {
   if (!t || n_chains < 0 || t->D < 1) return 0;
   const bool dense = t->kind == HMC_TARGET_DENSE;
-  if (hmc::big_path(dense, t->D)) return hmc::big_workspace_bytes(n_chains, t->D, dense);
+  if (hmc::big_path(dense, t->D)) return hmc::big_workspace_bytes(n_chains, t->D, dense, !k || k->minv_full);
   if (!dense) return 0;
   return hmc::dense_workspace_bytes(n_chains, t->D);
+}
+
+int64_t hmc_random_workspace_size(const hmc_target* t, int64_t n_chains) {
+  return hmc_random_workspace_size_ex(t, nullptr, n_chains);   // enough for either cov_p
 }
 
 int64_t hmc_nuts_workspace_size_ex(int32_t D, int64_t n_chains, int32_t d_max, int32_t iters_per_call,
@@ -318,6 +330,25 @@ int64_t hmc_nuts_workspace_size_ex(int32_t D, int64_t n_chains, int32_t d_max, i
 int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max) {
   return std::max(hmc_nuts_workspace_size_ex(D, n_chains, d_max, 32, 1),
                   hmc_nuts_workspace_size_ex(D, n_chains, d_max, 32, 0));
+}
+
+hmc_status hmc_nuts_iters_ws(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, const hmc_replay* r,
+                             hmc_state* st, void* workspace, int64_t workspace_bytes, void* stream) {
+  if (hmc_status e = check_schedule(t, k, s, false)) return e;
+  if (s->d_max < 1 || s->d_max > 15) return fail(HMC_EINVAL, "d_max must be in [1, 15]");
+  if (s->iter_end > s->iter_begin && s->n_chains > 0) {
+    // the sized workspace must cover this call: its Philox momenta drawn ahead (diagonal cov_p)
+    // for this call's iterations, or the tree vectors of the kernel this call takes
+    const int32_t pm = s->rng_mode == HMC_RNG_PHILOX && !k->minv_full ? 1 : 0;
+    const int64_t need = hmc_nuts_workspace_size_ex(t->D, s->n_chains, s->d_max, s->iter_end - s->iter_begin, pm);
+    if (need <= 0) return fail(HMC_EINVAL, "NUTS workspace: unsupported D=%d / d_max=%d", t->D, s->d_max);
+    if (workspace_bytes < need)
+      return fail(HMC_EINVAL, "NUTS workspace of %lld bytes; this call (D=%d, %lld chains, d_max=%d, %d iterations, "
+                  "%s momenta) needs %lld (hmc_nuts_workspace_size_ex)", (long long)workspace_bytes, t->D,
+                  (long long)s->n_chains, s->d_max, s->iter_end - s->iter_begin, pm ? "Philox" : "no pre-drawn",
+                  (long long)need);
+  }
+  return hmc_nuts_iters(t, k, s, r, st, workspace, stream);
 }
 
 hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, const hmc_replay* r,
@@ -442,14 +473,15 @@ hmc_status hmc_rowsum(const double* x, int64_t n_outer, int64_t outer_stride, in
 hmc_status hmc_variogram(const double* x, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
                          int64_t base, int32_t n, int32_t D, int32_t t0, int32_t t1, double* work, double* out,
                          void* stream) {
-  if (!x || !work || !out || n_chains < 1 || n < 1 || D < 1 || t0 < 1 || t1 <= t0 || t1 - t0 > 4096)
-    return fail(HMC_EINVAL, "bad arguments");
+  if (!x || !work || !out || n_chains < 1 || n < 1 || D < 1 || t0 < 1 || t1 <= t0 || t1 - t0 > kMaxLags)
+    return fail(HMC_EINVAL, "bad arguments (1 <= t0 < t1, t1 - t0 <= %d)", kMaxLags);
+  if (!hmc::diag_view_ok(n_chains, chain_stride, sample_stride, n, D, 2, 0, 0)) return view_too_large("hmc_variogram");
   return hip_status(hmc::launch_variogram(x, n_chains, chain_stride, sample_stride, base, n, D, t0, t1, work, out,
                                           (hipStream_t)stream),
-                    "hmc_variogram");
+                    "hmc_variogram (the view must keep one chain's samples within 1 GiB, include/hmc.h)");
 }
 
-static bool conv_tmax_ok(int32_t t) { return t >= 1 && t <= 4096; }
+static bool conv_tmax_ok(int32_t t) { return t >= 1 && t <= kMaxLags; }
 
 int64_t hmc_convergence_work_size(int64_t n_chains, int32_t D, int32_t tmax) {
   if (n_chains < 1 || D < 1 || !conv_tmax_ok(tmax)) return 0;
@@ -460,10 +492,26 @@ hmc_status hmc_convergence_sums(const double* x, int64_t n_chains, int64_t chain
                                 int64_t base, int32_t n, int32_t D, int32_t tmax, double* work, double* out,
                                 void* stream) {
   if (!x || !work || !out || n_chains < 1 || n < 2 || D < 1) return fail(HMC_EINVAL, "bad arguments");
-  if (!conv_tmax_ok(tmax)) return fail(HMC_EINVAL, "tmax must be in 1 .. 4096");
+  if (!conv_tmax_ok(tmax)) return fail(HMC_EINVAL, "tmax must be in 1 .. %d", kMaxLags);
+  if (!hmc::diag_view_ok(n_chains, chain_stride, sample_stride, n, D, 2, 0, 0))
+    return view_too_large("hmc_convergence_sums");
   return hip_status(hmc::launch_conv_fused(x, n_chains, chain_stride, sample_stride, base, n, D, tmax, work, out,
                                            (hipStream_t)stream),
                     "hmc_convergence_sums");
+}
+
+hmc_status hmc_half_sums(const double* window, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
+                         int32_t D, int32_t wrap, int32_t slot0, int32_t n, int32_t tmax, double* work, double* out,
+                         void* stream) {
+  if (!window || !work || !out || n_chains < 1 || n < 2 || D < 1 || slot0 < 0 || wrap < 0 ||
+      (wrap > 0 && (slot0 >= wrap || n > wrap)))
+    return fail(HMC_EINVAL, "bad arguments");
+  if (!conv_tmax_ok(tmax)) return fail(HMC_EINVAL, "tmax must be in 1 .. %d", kMaxLags);
+  if (!hmc::diag_view_ok(n_chains, chain_stride, sample_stride, n, D, 1, wrap, slot0))
+    return view_too_large("hmc_half_sums");
+  return hip_status(hmc::launch_half_sums(window, n_chains, chain_stride, sample_stride, D, wrap, slot0, n, tmax, work,
+                                          out, (hipStream_t)stream),
+                    "hmc_half_sums");
 }
 
 int64_t hmc_stream_work_size(int64_t n_chains, int32_t D, int32_t tmax) {

@@ -28,9 +28,17 @@ struct Src {
   int64_t chain_stride, sample_stride, base;
   int64_t n_chains;
   int n, D;
+  // series per chain: 2 = the split chains j = 2m + h of convergence_stats (half h starts h*n
+  // samples in); 1 = one series per chain (a completed half of a streaming window: series j =
+  // chain j, its sample s in window row (slot0 + s) % wrap, wrap 0 = row s)
+  int halves = 2;
+  int wrap = 0, slot0 = 0;
 };
 
+__host__ __device__ __forceinline__ int64_t n_series(const Src& s) { return s.halves * s.n_chains; }
+
 __device__ __forceinline__ const double* split_ptr(const Src& s, int64_t j, int smp) {
+  if (s.halves == 1) return s.x + s.base + j * s.chain_stride + (int64_t)smp * s.sample_stride;
   const int64_t m = j >> 1;
   const int h = (int)(j & 1);
   return s.x + s.base + m * s.chain_stride + (int64_t)(h * s.n + smp) * s.sample_stride;
@@ -183,7 +191,14 @@ __device__ __forceinline__ void static_for(F& f) {
 // 53 ms with the ragged rows masked instead of branched; 48 lags at two waves per SIMD spill).
 constexpr int kLagTL = HMC_LAG_TL;
 constexpr int kLagPF = HMC_LAG_PF;   // divides kLagTL
-constexpr int kLagRows = kLagTL + 4;   // partial rows per wave: std, mean - S, (mean - S)^2, lag n-1, lags
+// Tail lags: a first pass (mom) also sums the last `tail` <= kLagTail lags n - k, k = 1 .. tail, in
+// difference form, V_{n-k} = sum_{i<k} (y_{n-k+i} - y_i)^2 (k terms each: rows 0 .. tail-1 and the
+// last tail rows).  A complete pass then needs the lag groups only for lags 1 .. n - 1 - tail:
+// n = 99 (c4's halves) takes two groups of 48 and a tail of 2 instead of a third group that would
+// read every row again for one lag.
+constexpr int kLagTail = 8;
+// partial rows per wave: std, mean - S, (mean - S)^2, the tail lags n-1 .. n-kLagTail, the lag group
+constexpr int kLagRows = kLagTL + 3 + kLagTail;
 constexpr int kLagWaves = 8192;        // target waves per pass (4 rounds of 2 waves per SIMD)
 constexpr int kLagOOB = 0x40000000;    // buffer bound: lanes past the last series read zeros
 
@@ -193,7 +208,8 @@ struct LagArgs {
   int T;           // lags of this pass
   int G;           // lag groups, ceil(T / TL)
   int C, R;        // classes, replicas per class
-  int mom;         // group 0 sums the moments and lag n - 1 (first pass)
+  int mom;         // group 0 sums the moments and the tail lags (first pass)
+  int tail;        // mom: tail lags n-1 .. n-tail (1 <= tail <= kLagTail)
   int64_t NT;      // tiles of 64 series
   int rowb;        // bytes between samples (sample_stride * 8)
 };
@@ -211,7 +227,10 @@ __host__ __device__ inline int lag_gcd(int a, int b) {
 // stream itself; also the moments), else gofs > 0 (a second, delayed stream).  The two forms are
 // separate non-inlined functions so that each gets its own register allocation (one kernel
 // holding both spilled at 256 registers).
-template <int TL, int PF, bool Z>
+// WR: one series per chain in a circular window (Src::halves == 1, wrap > 0): sample s of every
+// series sits in window row (slot0 + s) % wrap, so row offsets wrap (scalar arithmetic per load);
+// the tile's buffer descriptor is based at the chain's window row 0.
+template <int TL, int PF, bool Z, bool WR>
 __device__ __forceinline__ void lag_wave(const LagArgs& a_, int W_, int g_, int c_, int r_, double* partial_) {
   // a function's arguments arrive in VGPRs: make every launch constant uniform again (SGPRs), so
   // that row and chunk tests stay scalar branches
@@ -223,12 +242,16 @@ __device__ __forceinline__ void lag_wave(const LagArgs& a_, int W_, int g_, int 
   a.s.n_chains = uni(a_.s.n_chains);
   a.s.n = uni(a_.s.n);
   a.s.D = uni(a_.s.D);
+  a.s.halves = WR ? 1 : uni(a_.s.halves);
+  a.s.wrap = WR ? uni(a_.s.wrap) : 0;
+  a.s.slot0 = WR ? uni(a_.s.slot0) : 0;
   a.L0 = uni(a_.L0);
   a.T = uni(a_.T);
   a.G = uni(a_.G);
   a.C = uni(a_.C);
   a.R = uni(a_.R);
   a.mom = uni(a_.mom);
+  a.tail = uni(a_.tail);
   a.NT = uni(a_.NT);
   a.rowb = uni(a_.rowb);
   const int W = uni(W_), g = uni(g_), c = uni(c_), r = uni(r_);
@@ -238,7 +261,17 @@ __device__ __forceinline__ void lag_wave(const LagArgs& a_, int W_, int g_, int 
   const int n = s.n, D = s.D;
   const int gofs = a.L0 + g * TL;
   const bool mom = Z && a.mom;                     // wave-uniform (Z: gofs == 0, group 0)
-  const int64_t m2 = 2 * s.n_chains;
+  const int64_t m2 = n_series(s);
+  // byte offset of sample `row` from a series' first window row (WR) or first sample
+  auto rowoff = [&](int row) -> int {
+    if constexpr (WR) {
+      int p = row + s.slot0;
+      p = p >= s.wrap ? p - s.wrap : p;
+      return p * a.rowb;
+    } else {
+      return row * a.rowb;
+    }
+  };
   // lane -> (split chain jj past the tile's first, dim d): the same for every tile of the class
   const int per = 64 / lag_gcd(D, 64);             // split chains per class period (64 C / D)
   const int d0 = (int)((64 * (int64_t)c) % D);
@@ -250,8 +283,12 @@ __device__ __forceinline__ void lag_wave(const LagArgs& a_, int W_, int g_, int 
   double v[TL];
 #pragma unroll
   for (int k = 0; k < TL; ++k) v[k] = 0.0;
-  double a_std = 0.0, a_m = 0.0, a_m2 = 0.0, a_last = 0.0;
-  const double Sd = s.x[s.base + d];               // shift of rows 1-2: the view's first sample
+  double a_std = 0.0, a_m = 0.0, a_m2 = 0.0;
+  double a_tail[kLagTail];
+#pragma unroll
+  for (int k = 0; k < kLagTail; ++k) a_tail[k] = 0.0;
+  // shift of rows 1-2: the view's first sample
+  const double Sd = s.x[s.base + (WR ? (int64_t)s.slot0 * s.sample_stride : 0) + d];
   if (gofs + 1 < n || mom) {
     // a tile's buffer descriptor and lane offset: split chain j0's first sample (wave-uniform) is the
     // base; lane offsets in bytes (host-checked below kLagOOB); lanes past the last series read
@@ -274,7 +311,7 @@ __device__ __forceinline__ void lag_wave(const LagArgs& a_, int W_, int g_, int 
     if (tau0 < a.NT) {
 #pragma unroll
       for (int p = 0; p < PF; ++p)
-        xn[p] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs_n, voff_n, (p < n ? p : n - 1) * a.rowb, 0));
+        xn[p] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs_n, voff_n, rowoff(p < n ? p : n - 1), 0));
     }
     for (int64_t tau = tau0; tau < a.NT; tau += (int64_t)a.C * a.R, j0 += jstep) {
       const bool valid = j0 + jj < m2;
@@ -291,23 +328,39 @@ __device__ __forceinline__ void lag_wave(const LagArgs& a_, int W_, int g_, int 
 #pragma unroll
         for (int p = 0; p < PF; ++p)
           xn[p] = __builtin_bit_cast(double,
-                                     __builtin_amdgcn_raw_buffer_load_b64(rs_n, voff_n, (p < n ? p : n - 1) * a.rowb, 0));
+                                     __builtin_amdgcn_raw_buffer_load_b64(rs_n, voff_n, rowoff(p < n ? p : n - 1), 0));
       }
       auto ldb = [&](int boff) -> double {         // sample at byte offset boff of the series
         return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, boff, 0));
       };
-      auto ld = [&](int row) -> double { return ldb(row * a.rowb); };
+      auto ld = [&](int row) -> double { return ldb(rowoff(row)); };
       // the rolling prefetch's next row, as a running byte offset (a scalar the compiler may not
-      // precompute per unrolled row: those products spilled the scalar file), clamped to row n - 1
+      // precompute per unrolled row: those products spilled the scalar file), clamped to row n - 1;
+      // WR: a running row number, clamped, then wrapped (and the delayed stream's row wrapped apart)
       const int last_off = (n - 1) * a.rowb;
       const int dly_off = gofs * a.rowb;
       int nxt = PF * a.rowb;
+      int nxr = PF;
+      int dly_o = 0;                               // WR: the delayed row's offset of the last next_off()
       auto next_off = [&]() {
-        int o = nxt < last_off ? nxt : last_off;
-        asm volatile("" : "+s"(o));
-        nxt += a.rowb;
-        asm volatile("" : "+s"(nxt));
-        return o;
+        if constexpr (WR) {
+          int rw = nxr < n - 1 ? nxr : n - 1;
+          asm volatile("" : "+s"(rw));
+          ++nxr;
+          asm volatile("" : "+s"(nxr));
+          if constexpr (!Z) dly_o = rowoff(rw - gofs);
+          return rowoff(rw);
+        } else {
+          int o = nxt < last_off ? nxt : last_off;
+          asm volatile("" : "+s"(o));
+          nxt += a.rowb;
+          asm volatile("" : "+s"(nxt));
+          return o;
+        }
+      };
+      auto dly_of = [&](int o) -> int {            // offset of the delayed stream's row
+        if constexpr (WR) return dly_o;
+        else return o - dly_off;
       };
       const double sh = xq[0];                      // row 0
       const double sh2 = 2.0 * sh;
@@ -344,7 +397,7 @@ __device__ __forceinline__ void lag_wave(const LagArgs& a_, int W_, int g_, int 
           {
             const int o = next_off();                // row min(s0 + i + PF, n - 1)
             xq[i % PF] = ldb(o);
-            if (DLY) xdq[i % PF] = ldb(o - dly_off);
+            if (DLY) xdq[i % PF] = ldb(dly_of(o));
           }
           // ragged rows past n: a uniform branch over the arithmetic only (the loads above are
           // unconditional, so no load result is a phi: the waitcnt pass keeps its counts)
@@ -403,8 +456,34 @@ __device__ __forceinline__ void lag_wave(const LagArgs& a_, int W_, int g_, int 
         const double e = mean - Sd;
         a_m += e;
         a_m2 = __builtin_fma(e, e, a_m2);
-        const double yl = ld(n - 1) - sh;          // lag n - 1: (x[n-1] - x[0])^2
-        a_last = __builtin_fma(yl, yl, a_last);
+        // the tail lags n - k, k = 1 .. tail, in difference form: y_0 = 0 (the shift), y_1 .. y_{tail-1}
+        // and the last tail samples, loaded together (clamped rows; unused values are masked)
+        const int K = a.tail;
+        double yl[kLagTail], yf[kLagTail];
+#pragma unroll
+        for (int j = 0; j < kLagTail; ++j) {
+          const int rl = n - 1 - j;
+          yl[j] = ld(j < K && rl > 0 ? rl : 0);     // y_{n-1-j} (+ sh)
+          yf[j] = ld(j < K ? j : 0);               // y_j (+ sh)
+        }
+#pragma unroll
+        for (int j = 0; j < kLagTail; ++j) {
+          yl[j] -= sh;
+          yf[j] -= sh;
+        }
+#pragma unroll
+        for (int k = 1; k <= kLagTail; ++k) {
+          if (k <= K) {                            // uniform
+            // V_{n-k} = sum_{i<k} (y_{n-k+i} - y_i)^2, y_{n-k+i} = yl[k-1-i]
+            double acc = 0.0;
+#pragma unroll
+            for (int i = 0; i < k; ++i) {
+              const double df = yl[k - 1 - i] - yf[i];
+              acc = __builtin_fma(df, df, acc);
+            }
+            a_tail[k - 1] += acc;
+          }
+        }
       }
     }
   }
@@ -412,12 +491,13 @@ __device__ __forceinline__ void lag_wave(const LagArgs& a_, int W_, int g_, int 
   out[0] = a_std;
   out[64] = a_m;
   out[128] = a_m2;
-  out[192] = a_last;
 #pragma unroll
-  for (int k = 0; k < TL; ++k) out[(4 + k) * 64] = v[k];
+  for (int k = 0; k < kLagTail; ++k) out[(3 + k) * 64] = a_tail[k];
+#pragma unroll
+  for (int k = 0; k < TL; ++k) out[(3 + kLagTail + k) * 64] = v[k];
 }
 
-template <int TL, int PF>
+template <int TL, int PF, bool WR>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_LAG_WPE, HMC_LAG_WPE))) void k_conv_series(LagArgs a,
                                                                                                double* partial) {
   const int W = blockIdx.x;
@@ -426,8 +506,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_LAG_WPE,
   const int cr = (u / a.G) * 8 + (W & 7);
   const int c = cr % a.C, r = cr / a.C;
   if (r >= a.R) return;                            // grid padding (never reduced)
-  if (a.L0 + g * TL == 0) lag_wave<TL, PF, true>(a, W, g, c, r, partial);
-  else lag_wave<TL, PF, false>(a, W, g, c, r, partial);
+  if (a.L0 + g * TL == 0) lag_wave<TL, PF, true, WR>(a, W, g, c, r, partial);
+  else lag_wave<TL, PF, false, WR>(a, W, g, c, r, partial);
 }
 
 // inter[(c * G + g) * kLagRows + row][l] = sum over the replicas r (in order) of the waves' lanes
@@ -463,17 +543,18 @@ __global__ __launch_bounds__(256) void k_lag_dims(LagArgs a, const double* __res
   int g = 0, prow;
   int t = 0;                                       // lag (0: a moment row)
   if (conv && orow < 3) prow = orow;
-  else if (conv && orow == nlag + 3) {
-    prow = 3;
-    t = a.s.n - 1;
-  } else {
-    const int k = skip + orow - (conv ? 3 : 0);    // lag index inside the pass
-    g = k / kLagTL;
-    prow = 4 + k % kLagTL;
-    t = a.L0 + 1 + k;
+  else {
+    t = (conv && orow == nlag + 3) ? a.s.n - 1 : a.L0 + 1 + skip + orow - (conv ? 3 : 0);
+    if (a.mom && t >= a.s.n - a.tail) {            // a tail lag (difference form, group 0)
+      prow = 3 + (a.s.n - 1 - t);
+    } else {
+      const int k = t - a.L0 - 1;                  // lag index inside the pass
+      g = k / kLagTL;
+      prow = 3 + kLagTail + k % kLagTL;
+    }
   }
   double acc = 0.0;
-  if (t < a.s.n && !(conv && orow == nlag + 3 && a.s.n < 2)) {
+  if (t < a.s.n && t >= 0 && g < a.G && !(conv && orow == nlag + 3 && a.s.n < 2)) {
     for (int c = 0; c < a.C; ++c) {
       int l = (int)(((int64_t)d - 64 * (int64_t)c) % D);
       if (l < 0) l += D;
@@ -804,6 +885,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T <= 16 ? 3
 
 int64_t rows_chunks(int64_t rows) { return (rows + kRowChunk - 1) / kRowChunk; }
 
+// G lag groups (and the tail) of a pass over lags L0 + 1 .. L0 + T.  A first pass (mom) asking for
+// every lag (T >= n - 2; lag n - 1 always comes from the tail) runs the groups up to lag
+// n - 1 - tail only and sums the rest, tail <= kLagTail lags, in difference form.
 LagArgs lag_args(const Src& s, int L0, int T, int mom) {
   LagArgs a{};
   a.s = s;
@@ -811,8 +895,17 @@ LagArgs lag_args(const Src& s, int L0, int T, int mom) {
   a.T = T;
   a.G = (T + kLagTL - 1) / kLagTL;
   a.mom = mom;
+  a.tail = mom ? 1 : 0;
+  if (mom && L0 == 0 && T >= s.n - 2 && s.n >= 2) {
+    const int need = s.n - 1 - kLagTail;           // lags the groups must cover at least
+    const int G = need > 0 ? (need + kLagTL - 1) / kLagTL : 1;
+    const int Tg = std::min(G * kLagTL, s.n - 2);
+    a.G = G;
+    a.T = Tg > 0 ? Tg : 0;
+    a.tail = s.n - 1 - a.T;
+  }
   a.C = s.D / lag_gcd(s.D, 64);
-  a.NT = (2 * s.n_chains * (int64_t)s.D + 63) / 64;
+  a.NT = (n_series(s) * (int64_t)s.D + 63) / 64;
   const int64_t per_class = (a.NT + a.C - 1) / a.C;
   const int64_t R = (kLagWaves + (int64_t)a.C * a.G - 1) / ((int64_t)a.C * a.G);
   a.R = (int)(R < per_class ? (R < 1 ? 1 : R) : per_class);
@@ -825,23 +918,55 @@ int64_t lag_work(const LagArgs& a) {
   return lag_grid(a) * kLagRows * 64 + (int64_t)a.C * a.G * kLagRows * 64;
 }
 
+// Work (doubles) that any pass of at most T lags (L0 = 0, n unknown: a complete first pass may take
+// fewer groups than ceil(T / TL)) over n_chains chains of D dims needs: the largest over the group
+// counts it could run.
+int64_t lag_work_bound(int64_t n_chains, int D, int T, int mom) {
+  int64_t w = 0;
+  const int Gmax = (T + kLagTL - 1) / kLagTL;
+  for (int G = 1; G <= Gmax; ++G) {
+    Src s{nullptr, 0, 0, 0, n_chains, 2, D};
+    LagArgs a = lag_args(s, 0, G * kLagTL, 0);   // geometry of G groups (pairs: the most series)
+    a.mom = mom;
+    w = std::max(w, lag_work(a));
+  }
+  return w;
+}
+
 // One read of the samples: lags L0 + 1 .. L0 + T (group 0 also the moments when mom), reduced into
 // out (conv layout or lags only, from lag L0 + 1 + skip, nlag lags).
+// Lane offsets (bytes from a tile's first series) and row offsets must stay inside the buffer
+// bound kLagOOB (1 GiB): a tile spans at most 64 / D + 2 series; the second half of a chain starts
+// n * sample_stride after its first (chain_stride >= that for every q_chain view).  So one chain's
+// samples (its stride) must stay well within 1 GiB: e.g. D = 1000 up to ~40,000 stored samples per
+// chain, D = 100 up to ~400,000 (hmc_amd.diagnostics splits larger views by dimension).
+bool lag_view_ok(const Src& s) {
+  const int64_t cs = s.chain_stride, ss = s.sample_stride;
+  if (ss < 1 || ss * 8 > 0x7FFFFFFF || s.D < 1) return false;
+  if (s.halves == 2) {
+    if (cs < (int64_t)s.n * ss) return false;
+    const int64_t span = ((64 / s.D + 2) / 2 + 1) * cs + (int64_t)s.n * ss + s.D;   // doubles
+    return (span + (int64_t)s.n * ss) * 8 < kLagOOB;
+  }
+  // one series per chain: a tile spans at most 64 / D + 2 chains; rows up to the window's last
+  const bool wr = s.wrap > 0;
+  const int64_t rows = wr ? (int64_t)s.wrap : (int64_t)s.n;
+  if (wr && (s.slot0 < 0 || s.slot0 >= s.wrap || s.n > s.wrap)) return false;
+  const int64_t span = (64 / s.D + 2) * cs + s.D;
+  return (span + rows * ss) * 8 < kLagOOB;
+}
+
 hipError_t launch_lags(const Src& s, int L0, int T, int mom, int conv, int skip, int nlag, double* work, double* out,
                        hipStream_t st) {
   if (T < 1 || L0 < 0 || L0 % kLagPF != 0) return hipErrorInvalidValue;
-  // lane offsets (bytes from a tile's first split chain) and row offsets must stay inside the
-  // buffer bound: at most 64 / D + 2 split chains per tile; the second half of a chain starts
-  // n * sample_stride after its first (chain_stride >= that for every q_chain view)
-  const int64_t cs = s.chain_stride, ss = s.sample_stride;
-  if (cs < (int64_t)s.n * ss || ss < 1 || ss * 8 > 0x7FFFFFFF) return hipErrorInvalidValue;
-  const int64_t span = ((64 / s.D + 2) / 2 + 1) * cs + (int64_t)s.n * ss + s.D;   // doubles
-  if ((span + (int64_t)s.n * ss) * 8 >= kLagOOB) return hipErrorInvalidValue;
+  if (!lag_view_ok(s)) return hipErrorInvalidValue;
+  const bool wr = s.halves == 1 && s.wrap > 0;
   const LagArgs a = lag_args(s, L0, T, mom);
   const int64_t grid = lag_grid(a);
   double* partial = work;
   double* inter = work + grid * kLagRows * 64;
-  k_conv_series<kLagTL, kLagPF><<<(unsigned)grid, 64, 0, st>>>(a, partial);
+  if (wr) k_conv_series<kLagTL, kLagPF, true><<<(unsigned)grid, 64, 0, st>>>(a, partial);
+  else k_conv_series<kLagTL, kLagPF, false><<<(unsigned)grid, 64, 0, st>>>(a, partial);
   if (hipError_t e = hipGetLastError()) return e;
   const int64_t ni = (int64_t)a.C * a.G * kLagRows * 64;
   k_lag_classes<<<(unsigned)((ni + 255) / 256), 256, 0, st>>>(a, partial, inter);
@@ -854,6 +979,11 @@ hipError_t launch_lags(const Src& s, int L0, int T, int mom, int conv, int skip,
 }  // namespace
 
 int64_t diag_rowsum_work(int64_t rows, int D) { return rows_chunks(rows) * D; }
+
+bool diag_view_ok(int64_t n_chains, int64_t cs, int64_t ss, int n, int D, int halves, int wrap, int slot0) {
+  Src s{nullptr, cs, ss, 0, n_chains, n, D, halves, wrap, slot0};
+  return lag_view_ok(s);
+}
 
 int64_t diag_variogram_work(int64_t n_chains, int D, int nlags) {
   Src s{nullptr, 0, 0, 0, n_chains, 2, D};
@@ -880,14 +1010,18 @@ hipError_t launch_rowsum(const double* x, int64_t n_outer, int64_t os, int64_t n
   return hipGetLastError();
 }
 
-int64_t diag_conv_work(int64_t n_chains, int D, int T) {
-  Src s{nullptr, 0, 0, 0, n_chains, 2, D};
-  return lag_work(lag_args(s, 0, T, 1));
-}
+int64_t diag_conv_work(int64_t n_chains, int D, int T) { return lag_work_bound(n_chains, D, T, 1); }
 
 hipError_t launch_conv_fused(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int64_t base, int n, int D,
                              int T, double* work, double* out, hipStream_t st) {
   Src s{x, cs, ss, base, n_chains, n, D};
+  return launch_lags(s, 0, T, 1, 1, 0, T, work, out, st);
+}
+
+hipError_t launch_half_sums(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int D, int wrap, int slot0,
+                            int n, int T, double* work, double* out, hipStream_t st) {
+  Src s{x, cs, ss, 0, n_chains, n, D, 1, wrap, slot0};
+  if (wrap <= 0) s.base = (int64_t)slot0 * ss;   // no wrap: sample s in row slot0 + s
   return launch_lags(s, 0, T, 1, 1, 0, T, work, out, st);
 }
 

@@ -112,7 +112,7 @@ struct BigArgs {
   double* E0;    // [n] energy at the start of the current iteration
 };
 bool big_path(int kind_dense, int D);
-int64_t big_workspace_bytes(int64_t n, int D, bool dense);
+int64_t big_workspace_bytes(int64_t n, int D, bool dense, bool full_mass);
 BigArgs big_args(const RandArgs& a, void* ws, bool dense);
 hipError_t launch_big_init(const BigArgs& b, bool dense, bool replay, hipStream_t s);
 hipError_t launch_big_iters(const BigArgs& b, bool dense, bool exact, bool replay, hipStream_t s);
@@ -142,11 +142,15 @@ hipError_t launch_rng_normals(uint32_t k0, uint32_t k1, int64_t chain0, int64_t 
 
 // Diagnostics (hmc_diag.hip).
 int64_t diag_rowsum_work(int64_t rows, int D);
+// whether the lag kernel's 32-bit buffer offsets cover a strided view (hmc_diag.hip lag_view_ok)
+bool diag_view_ok(int64_t n_chains, int64_t cs, int64_t ss, int n, int D, int halves, int wrap, int slot0);
 int64_t diag_variogram_work(int64_t n_chains, int D, int nlags);
 int64_t diag_stream_groups(int64_t n_chains);
 int64_t diag_conv_work(int64_t n_chains, int D, int T);
 hipError_t launch_conv_fused(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int64_t base, int n, int D,
                              int T, double* work, double* out, hipStream_t st);
+hipError_t launch_half_sums(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int D, int wrap, int slot0,
+                            int n, int T, double* work, double* out, hipStream_t st);
 hipError_t launch_stream_accum(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int D, int wrap, int slot0,
                                int carry, int rows, int64_t pos0, int n, double* shift, double* s1, double* s2, int T,
                                double* vpart, double* vsum, hipStream_t st);

@@ -65,11 +65,15 @@ SYMBOLS = {
                                              ctypes.c_int64, ctypes.c_int32, c_dp, c_dp, c_dp, ctypes.c_int32, c_dp,
                                              c_dp, c_dp]),
     "hmc_random_workspace_size": (ctypes.c_int64, [ctypes.POINTER(Target), ctypes.c_int64]),
+    "hmc_random_workspace_size_ex": (ctypes.c_int64, [ctypes.POINTER(Target), ctypes.POINTER(Kinetic),
+                                                      ctypes.c_int64]),
     "hmc_nuts_workspace_size": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32]),
     "hmc_nuts_workspace_size_ex": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                                     ctypes.c_int32]),
     "hmc_nuts_iters": (ctypes.c_int, [ctypes.POINTER(Target), ctypes.POINTER(Kinetic), ctypes.POINTER(Schedule),
                                       ctypes.POINTER(Replay), ctypes.POINTER(State), c_dp, c_dp]),
+    "hmc_nuts_iters_ws": (ctypes.c_int, [ctypes.POINTER(Target), ctypes.POINTER(Kinetic), ctypes.POINTER(Schedule),
+                                         ctypes.POINTER(Replay), ctypes.POINTER(State), c_dp, ctypes.c_int64, c_dp]),
     "hmc_leapfrog": (ctypes.c_int, [ctypes.POINTER(Target), ctypes.POINTER(Kinetic), ctypes.c_int64, c_dp, c_dp,
                                     c_dp, c_dp, ctypes.c_int32, c_dp]),
     "hmc_energy": (ctypes.c_int, [ctypes.POINTER(Target), ctypes.POINTER(Kinetic), ctypes.c_int64, c_dp, c_dp,
@@ -85,6 +89,9 @@ SYMBOLS = {
     "hmc_convergence_work_size": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
     "hmc_convergence_sums": (ctypes.c_int, [c_dp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                             ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_dp, c_dp, c_dp]),
+    "hmc_half_sums": (ctypes.c_int, [c_dp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
+                                     ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_dp, c_dp,
+                                     c_dp]),
     "hmc_variogram_work_size": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
     "hmc_variogram": (ctypes.c_int, [c_dp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                      ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_dp, c_dp,

@@ -107,37 +107,45 @@ def convergence_sums(sp, tmax):
 
 
 FIRST_PASS_LAGS = 96
+COMPLETE_PASS_LAGS = 256
 
 
 def conv_tmax(n):
     """Lags 1..tmax of the one-pass sums for split chains of n samples.  The pass always adds lag
-    n - 1 (one square per split chain), so tmax = n - 2 makes it complete: every lag t < n, the
-    whole ESS loop, in one read of the samples (n = 50, the bench window: 48 lags).  Longer chains
-    take the first FIRST_PASS_LAGS lags; dimensions whose criterion has not fired by then read
-    all the remaining lags in ONE more pass (hmc_variogram), so a slow-mixing window is read at
-    most twice and a fast-mixing one once, without the O(n^2) cost of every lag."""
-    return max(1, min(n - 2, FIRST_PASS_LAGS))
+    n - 1, so tmax = n - 2 makes it complete: every lag t < n, the whole ESS loop, in one read of the
+    samples (the kernel's lag groups run to n - 1 - tail, the last tail <= 8 lags are summed in
+    difference form).  Windows of up to COMPLETE_PASS_LAGS + 1 samples per half take that complete
+    pass (n = 50, the bench window; n = 200, c3's: no second read whatever the mixing).  Longer
+    chains take the first FIRST_PASS_LAGS lags; dimensions whose criterion has not fired by then
+    read the remaining lags in ONE more pass (hmc_variogram), without the O(n^2) cost of every lag
+    for fast-mixing ones."""
+    if n - 1 <= COMPLETE_PASS_LAGS:
+        return max(1, n - 2)
+    return FIRST_PASS_LAGS
 
 
-def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
-    """utils.py:77-159 on the GPU.  q_chain: (Nchain, Niter, D) NumPy array or CUDA tensor
-    (views such as q_chain_device[:, 1:, :] are read in place).  Returns (R, n_eff) NumPy.
+def _fits(cs, ss, n, D):
+    """Whether the lag kernel's 32-bit buffer offsets cover a view (hmc_diag.hip lag_view_ok,
+    pairs of halves): one chain's span must stay within 1 GiB."""
+    if cs < n * ss:
+        return False
+    span = ((64 // D + 2) // 2 + 1) * cs + n * ss + D
+    return (span + n * ss) * 8 < (1 << 30)
 
-    One pass over the samples gives every per-dimension sum R-hat needs and the variogram of every
-    lag t < n up to conv_tmax(n), and of lag n - 1 (hmc_convergence_sums); the ESS termination
-    (utils.py:130-157) runs vectorised over the dimensions on the host, and only dimensions whose
-    criterion has not fired by then (n > 98 and slow mixing) read the remaining lags, all in one
-    more pass (hmc_variogram).  Ranks all-reduce the per-dimension sums: two rounds, B needs the global
-    mean."""
-    sp = _Split(q_chain, thin_rate, warm_up_num)
-    n, D = sp.n, sp.D
-    dev = sp.t.device
-    tmax = conv_tmax(n)
-    sums = convergence_sums(sp, tmax)
-    S = sp.t[0, warm_up_num, :].to(torch.float64)                       # the kernels' shift x[base + d]
-    # (a strided view of the stored sample: no copy of a non-contiguous q_chain view, and the
-    # right elements for dim-sliced views whose row stride is not D)
-    m_loc = 2 * sp.Nchain
+
+def _view_fits(sp):
+    return _fits(sp.cs, sp.ss, sp.n, sp.D)
+
+
+def rhat_ess_from_sums(sums, S, m_loc, n, tmax, group=None):
+    """R-hat and the ESS loop (utils.py:109-157) from one-pass sums in the hmc_convergence_sums
+    layout (sums (4 + tmax, D): sum_j std_j, sum_j (mean_j - S), sum_j (mean_j - S)^2, the variogram
+    sums of lags 1..tmax, that of lag n - 1) over this rank's m_loc split chains, S their shift.
+    Ranks all-reduce the per-dimension sums: two rounds, B needs the global mean.
+    Returns (R numpy, n_eff numpy, need, Vt, var_h, m): `need` flags the dims whose criterion reads a
+    lag beyond those given (n_eff NaN there), Vt the variogram values used."""
+    D = sums.shape[1]
+    dev = sums.device
     # round 1: sum_j std_j, sum_j mean_j (= shifted sum + m S), variogram sums, split-chain count
     r1 = torch.cat([sums[0:1], (sums[1] + m_loc * S)[None], sums[3:],
                     torch.full((1, D), float(m_loc), dtype=torch.float64, device=dev)])
@@ -154,15 +162,41 @@ def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
     R = torch.sqrt(var / W)                                             # :126
     v = r1[2:3 + tmax].cpu().numpy()                                    # lags 1..tmax, then lag n - 1
     var_h = var.cpu().numpy()
-    # ---- ESS (utils.py:128-157), vectorised over dims; more lags only where still undecided
+    # ---- ESS (utils.py:128-157), vectorised over dims
     lmax = max(n - 1, 2)                                                # lags t < n exist
     T = min(tmax, lmax)
     v = np.vstack([v[:T], v[tmax:tmax + 1]]) if T == n - 2 else v[:T]  # + lag n - 1: complete
     T = v.shape[0]
     Vt = v / (m * (n - np.arange(1, T + 1)))[:, None]                   # utils.py:177
     n_eff, need = ess_vectorised(Vt, var_h, n, m, complete=T >= lmax)
+    return R.cpu().numpy(), n_eff, need, Vt, var_h, m
+
+
+def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
+    """utils.py:77-159 on the GPU.  q_chain: (Nchain, Niter, D) NumPy array or CUDA tensor
+    (views such as q_chain_device[:, 1:, :] are read in place).  Returns (R, n_eff) NumPy.
+
+    One pass over the samples gives every per-dimension sum R-hat needs and the variogram of every
+    lag t < n up to conv_tmax(n), and of lag n - 1 (hmc_convergence_sums); the ESS termination
+    (utils.py:130-157) runs vectorised over the dimensions on the host, and only dimensions whose
+    criterion has not fired by then (long, slow-mixing windows) read the remaining lags, in one
+    more pass (hmc_variogram).  Ranks all-reduce the per-dimension sums: two rounds, B needs the
+    global mean.  Views whose chains span more than the lag kernel's 1 GiB offsets (very long stored
+    runs) are processed as contiguous copies of dimension slices (every statistic is per dimension)."""
+    sp = _Split(q_chain, thin_rate, warm_up_num)
+    if not _view_fits(sp):
+        return _convergence_stats_sliced(sp, thin_rate, warm_up_num, group)
+    n, D = sp.n, sp.D
+    dev = sp.t.device
+    tmax = conv_tmax(n)
+    sums = convergence_sums(sp, tmax)
+    S = sp.t[0, warm_up_num, :].to(torch.float64)                       # the kernels' shift x[base + d]
+    # (a strided view of the stored sample: no copy of a non-contiguous q_chain view, and the
+    # right elements for dim-sliced views whose row stride is not D)
+    R, n_eff, need, Vt, var_h, m = rhat_ess_from_sums(sums, S, 2 * sp.Nchain, n, tmax, group)
+    lmax = max(n - 1, 2)
     LAST_INFO.clear()
-    LAST_INFO.update(mode="stored", tmax=tmax, lags=T, fallback_dims=int(need.sum()), fallback_passes=0,
+    LAST_INFO.update(mode="stored", tmax=tmax, lags=Vt.shape[0], fallback_dims=int(need.sum()), fallback_passes=0,
                      truncated_dims=0)
     if need.any():
         # the dims whose criterion reads lags > T: gather their columns once (one strided read of
@@ -186,7 +220,32 @@ def convergence_stats(q_chain, thin_rate=5, warm_up_num=0, group=None):
         assert not need2.any()
         n_eff[idx] = ne
         LAST_INFO["lags"] = Vs.shape[0]
-    return R.cpu().numpy(), n_eff
+    return R, n_eff
+
+
+def _convergence_stats_sliced(sp, thin_rate, warm_up_num, group):
+    """convergence_stats of a view too long for the lag kernel's offsets: contiguous copies of
+    dimension slices small enough to fit, each its own pass (R-hat and ESS are per dimension)."""
+    t = sp.t
+    N, L, D = t.shape
+    rows = len(range(warm_up_num, L, thin_rate))
+    per = D
+    while per > 1 and not _fits(rows * per, per, rows // 2, per):     # a contiguous (N, rows, per) copy
+        per = (per + 1) // 2
+    if not _fits(rows * per, per, rows // 2, per):
+        raise NotImplementedError("convergence_stats: %d samples per chain exceed the lag kernel's offsets" % rows)
+    R, ne = np.empty(D), np.empty(D)
+    info = None
+    for d0 in range(0, D, per):
+        d1 = min(D, d0 + per)
+        sub = t[:, warm_up_num::thin_rate, d0:d1].contiguous()
+        R[d0:d1], ne[d0:d1] = convergence_stats(sub, thin_rate=1, warm_up_num=0, group=group)
+        info = dict(LAST_INFO) if info is None else {k: (info[k] + LAST_INFO[k] if k in ("fallback_dims",
+                                                                                      "fallback_passes") else info[k])
+                                                     for k in info}
+    LAST_INFO.clear()
+    LAST_INFO.update(info, slices=(D + per - 1) // per)
+    return R, ne
 
 
 LAST_INFO = {}   # what the last convergence_stats call read: fused lags, fallback dims and passes
@@ -345,31 +404,106 @@ def combine_split_stats(mean, std, vsum, n, group=None, info=None):
 
 
 class StreamingDiagnostics:
-    """convergence_stats (utils.py:77-159) of q_chain[:, 1:, :] without storing q_chain:
-    samples arrive in windows (hmc_stream_accumulate) and only per-chain/half moments plus
-    variogram lag sums for lags <= tmax are kept.  Exact for R-hat; ESS uses lags <= tmax
-    (the reference's sum stops earlier whenever its criterion fires within tmax).
+    """convergence_stats (utils.py:77-159) of q_chain[:, 1:, :] without storing q_chain.
+
+    Two modes, chosen by the sampler loop that feeds the rows (RandomEngine.run_streaming):
+      * "exact": each split half is fed once it is complete and still whole in the circular window
+        (add_half -> hmc_half_sums: the one-read lag kernel over that half of every chain, every lag
+        1 .. n-1).  R-hat and ESS are then the reference estimator exactly (truncated_dims 0), and
+        the window only has to hold one half plus a launch's rows.
+      * "stream": halves longer than the window arrive in segments (update ->
+        hmc_stream_accumulate): per-chain/half moments plus variogram lag sums for lags <= tmax.
+        Exact for R-hat; the ESS sum stops at lag tmax where the reference's criterion has not
+        fired by then (counted in info["truncated_dims"]).
 
     n_samples = L_chain - 1 (rows after the dropped first row, Q16)."""
 
-    def __init__(self, n_chains, D, n_samples, tmax=16, device=None):
+    def __init__(self, n_chains, D, n_samples, tmax=16, device=None, mode=None):
         self.N, self.D, self.tmax = int(n_chains), int(D), int(tmax)
         self.n = int(n_samples) // 2                                    # utils.py:102
         assert self.n >= 2, "need at least 4 samples per chain"
+        assert mode in (None, "exact", "stream")
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.device = dev
-        z = lambda *s: torch.zeros(s, dtype=torch.float64, device=dev)  # noqa: E731
-        self.shift, self.s1, self.s2 = z(self.N, 2, D), z(self.N, 2, D), z(self.N, 2, D)
-        self.vsum = z(self.tmax, D)
-        L = H.lib()
-        self.work = z(max(1, L.hmc_stream_work_size(self.N, D, self.tmax)))
+        self._z = lambda *s: torch.zeros(s, dtype=torch.float64, device=dev)  # noqa: E731
         self.pos = 0                                                    # samples consumed
+        self.mode = mode                                                # "exact" | "stream"; None: the feeder picks
+        self._stream_state = None
+        self.halves = []                                                # exact: halves added, in order
+        self.xsums = None                                               # exact: sums about xshift
+        self.xshift = None
+
+    # stream-mode state, allocated on first use
+    @property
+    def shift(self):
+        return self._state()[0]
+
+    @property
+    def s1(self):
+        return self._state()[1]
+
+    @property
+    def s2(self):
+        return self._state()[2]
+
+    @property
+    def vsum(self):
+        return self._state()[3]
+
+    def _state(self):
+        if self._stream_state is None:
+            N, D, z = self.N, self.D, self._z
+            self.work = z(max(1, H.lib().hmc_stream_work_size(N, D, self.tmax)))
+            self._stream_state = (z(N, 2, D), z(N, 2, D), z(N, 2, D), z(self.tmax, D))
+        return self._stream_state
+
+    def _set_mode(self, mode):
+        if self.mode is None:
+            self.mode = mode
+        elif self.mode != mode:
+            raise AssertionError("StreamingDiagnostics: a run feeds either whole halves or segments")
+
+    def exact_lags(self):
+        """tmax of the exact halves' sums: every lag 1 .. n-1 (n - 2 plus the lag n - 1 row)."""
+        return max(1, self.n - 2)
+
+    def add_half(self, window, h, slot0):
+        """Exact mode: split half h (positions h*n .. h*n + n - 1) of every chain is complete in the
+        circular window (N, W, D), its first sample in row slot0 (rows wrap at W).  One read of those
+        rows gives its moments and every lag (hmc_half_sums), accumulated about a common shift."""
+        self._set_mode("exact")
+        assert window.stride(2) == 1 and window.shape[0] == self.N and window.shape[2] == self.D
+        assert h == len(self.halves), "halves must be added in order"
+        assert self.n <= window.shape[1], "the window must hold a whole half"
+        T = self.exact_lags()
+        L = H.lib()
+        work = self._z(max(1, L.hmc_convergence_work_size(self.N, self.D, T)))
+        out = self._z(4 + T, self.D)
+        Wr = window.shape[1]
+        H.check(L.hmc_half_sums(window.data_ptr(), self.N, window.stride(0), window.stride(1), self.D, Wr,
+                                int(slot0) % Wr, self.n, T, H.ptr(work), H.ptr(out), _stream(window)),
+                "hmc_half_sums")
+        S = window[0, int(slot0) % Wr, :].to(torch.float64).clone()     # the kernel's shift: chain 0's sample 0
+        if self.xsums is None:
+            self.xsums, self.xshift = out, S
+        else:
+            # re-centre onto the first half's shift: sum (mean - S0) = sum (mean - S) + N (S - S0), ...
+            dS = S - self.xshift
+            x = self.xsums
+            x[2] += out[2] + 2.0 * dS * out[1] + self.N * dS * dS
+            x[1] += out[1] + self.N * dS
+            x[0] += out[0]
+            x[3:] += out[3:]
+        self.halves.append(h)
+        self.pos = (h + 1) * self.n
 
     def update(self, window, carry, rows, slot0=0):
         """window: (N, W, D) device tensor (any chain/sample strides, dims contiguous), circular:
         the `carry` samples before the new ones and then the `rows` new samples sit in rows
         slot0, slot0 + 1, ... (mod W)."""
         assert window.stride(2) == 1 and window.shape[0] == self.N and window.shape[2] == self.D
+        self._set_mode("stream")
+        self._state()
         H.check(H.lib().hmc_stream_accumulate(window.data_ptr(), self.N, window.stride(0), window.stride(1), self.D,
                                               window.shape[1], int(slot0), int(carry), int(rows), self.pos, self.n,
                                               H.ptr(self.shift),
@@ -385,10 +519,21 @@ class StreamingDiagnostics:
         return mean.reshape(2 * self.N, self.D), torch.sqrt(torch.clamp(var, min=0.0)).reshape(2 * self.N, self.D)
 
     def finish(self, group=None):
-        """(R, n_eff).  self.info (and diagnostics.LAST_INFO) then hold tmax, the lags used and
-        truncated_dims: how many dimensions' ESS criterion had not fired by lag tmax, i.e. whose
-        n_eff differs from the reference's (0 = every n_eff is the reference's)."""
+        """(R, n_eff).  self.info (and diagnostics.LAST_INFO) then hold the mode, the lags used and
+        truncated_dims: how many dimensions' ESS criterion had not fired by the last lag available,
+        i.e. whose n_eff differs from the reference's (0 = every n_eff is the reference's; always 0
+        in exact mode)."""
         assert self.pos >= 2 * self.n, "not all split-chain samples were fed"
+        if self.mode == "exact":
+            assert self.halves == [0, 1]
+            T = self.exact_lags()
+            R, n_eff, need, Vt, _, _ = rhat_ess_from_sums(self.xsums, self.xshift, 2 * self.N, self.n, T, group)
+            assert not need.any()
+            info = dict(mode="streaming-exact", lags=int(Vt.shape[0]), truncated_dims=0, n_half=int(self.n))
+            self.info = info
+            LAST_INFO.clear()
+            LAST_INFO.update(info)
+            return R, n_eff
         mean, std = self.moments()
         info = dict(mode="streaming", tmax=self.tmax)
         out = combine_split_stats(mean, std, self.vsum, self.n, group, info=info)

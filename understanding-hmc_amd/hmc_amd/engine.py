@@ -89,9 +89,17 @@ class RandomEngine:
                          H.ptr(self.decision), self.n_save, self.traj_stride)
         # dense targets: scratch for L-ordered MFMA tiles (chains sorted by trajectory length
         # every iteration; same results, no lane idling through a longer trajectory).  The large-D
-        # path (dense D > 128, diagonal D > 2048) keeps its chain state there: always allocated.
+        # path (dense D > 128, diagonal D > 2048) keeps its chain state there: always allocated (a
+        # NUTS run only needs it for hmc_chain_init's start energies, random_ws=False: sized for the
+        # init alone, i.e. without the full-cov_p products unless cov_p is full)
         big = (D > 128) if kind == H.HMC_TARGET_DENSE else ((D + 1) // 2 > 16 * 64)
-        nbytes = H.lib().hmc_random_workspace_size(self.T, self.N) if (order_tiles or big) else 0
+        L_ = H.lib()
+        if big:
+            nbytes = L_.hmc_random_workspace_size_ex(self.T, self.K, self.N)
+        elif order_tiles and random_ws:
+            nbytes = L_.hmc_random_workspace_size(self.T, self.N)
+        else:
+            nbytes = 0
         self._order = torch.zeros((nbytes + 3) // 4, dtype=torch.int32, device=dev) if nbytes > 0 else None
         self.S.order = H.ptr(self._order)
         self._replay = None
@@ -156,7 +164,14 @@ class RandomEngine:
         N, D, T = self.N, self.D, diag.tmax
         feed = step if feed is None else int(feed)
         assert feed >= step and feed % step == 0, "feed must be a multiple of step"
-        W = T + (feed + step) // self.thin + 2
+        # exact mode (every lag of the reference's ESS loop) whenever a whole split half fits in no
+        # more window than the segment mode would use: each half is fed once complete, from a
+        # window of n + ceil(step/thin) + 2 rows; otherwise segments of `feed` iterations
+        exact = diag.mode == "exact" or (diag.mode is None and diag.n <= T + feed // self.thin)
+        if exact:
+            W = diag.n + -(-step // self.thin) + 2
+        else:
+            W = T + (feed + step) // self.thin + 2
         st = getattr(self, "_stream", None)
         if st is not None and st[0] is diag and st[1].shape[1] != W and diag.pos > 0:
             # the window holds the variogram carry (and possibly written but unfed rows) at
@@ -177,6 +192,13 @@ class RandomEngine:
             if events is not None:
                 events[1].record(torch.cuda.current_stream(self.device))
             done = self.L_chain if b - 1 == self.n_iter else max(0, (b - self.warm_up) // self.thin)
+            if exact:
+                # split half h = chain rows 1 + h n .. (h + 1) n, whole in the window once complete
+                h = len(diag.halves)
+                while h < 2 and done >= 1 + (h + 1) * diag.n:
+                    diag.add_half(win, h, (1 + h * diag.n) % W)
+                    h += 1
+                continue
             if done > next_row and (done - next_row >= feed // self.thin or b - 1 == self.n_iter):
                 carry = min(T, next_row - 1)
                 diag.update(win, carry, done - next_row, slot0=(next_row - carry) % W)
@@ -216,11 +238,17 @@ class RandomEngine:
         if self._order is not None:
             arr["order_ws"] = self._order                   # dense: tile order + gradient cache of q
         if diag is not None:
-            arr.update(diag_shift=diag.shift, diag_s1=diag.s1, diag_s2=diag.s2, diag_vsum=diag.vsum)
+            if diag.mode == "exact":
+                if diag.xsums is not None:
+                    arr.update(diag_xsums=diag.xsums, diag_xshift=diag.xshift)
+            else:
+                arr.update(diag_shift=diag.shift, diag_s1=diag.s1, diag_s2=diag.s2, diag_vsum=diag.vsum)
             st = getattr(self, "_stream", None)
             if st is not None and st[0] is diag:
-                arr["window"] = st[1]                       # carry rows of the variogram lags
-        meta = dict(self._meta(), it_next=int(it_next), diag_pos=None if diag is None else diag.pos)
+                arr["window"] = st[1]                       # rows of an open half / the lag carry
+        meta = dict(self._meta(), it_next=int(it_next), diag_pos=None if diag is None else diag.pos,
+                    diag_mode=None if diag is None else diag.mode,
+                    diag_halves=None if diag is None else list(diag.halves))
         np.savez(path, meta=np.array(json.dumps(meta)), **{k: v.cpu().numpy() for k, v in arr.items()})
 
     def restore(self, path, diag=None):
@@ -240,9 +268,16 @@ class RandomEngine:
             if self._order is not None and "order_ws" not in z.files:
                 self._order.zero_()                         # no cached gradient: recomputed from q
             if diag is not None:
-                for k, t in (("diag_shift", diag.shift), ("diag_s1", diag.s1), ("diag_s2", diag.s2),
-                             ("diag_vsum", diag.vsum)):
-                    t.copy_(torch.as_tensor(z[k]).to(self.device))
+                diag.mode = meta.get("diag_mode")
+                diag.halves = list(meta.get("diag_halves") or [])
+                if diag.mode == "exact":
+                    if "diag_xsums" in z.files:
+                        diag.xsums = torch.as_tensor(z["diag_xsums"]).to(self.device)
+                        diag.xshift = torch.as_tensor(z["diag_xshift"]).to(self.device)
+                elif "diag_shift" in z.files:
+                    for k, t in (("diag_shift", diag.shift), ("diag_s1", diag.s1), ("diag_s2", diag.s2),
+                                 ("diag_vsum", diag.vsum)):
+                        t.copy_(torch.as_tensor(z[k]).to(self.device))
                 diag.pos = int(meta["diag_pos"])
                 if "window" in z.files:
                     self._stream = [diag, torch.as_tensor(z["window"]).to(self.device)]
@@ -288,6 +323,9 @@ class NutsEngine(RandomEngine):
                                 H.ptr(self._streams[2]), tape.shape[1])
 
     def run(self, it0, it1):
-        assert it1 - it0 <= self.iters_per_call, "NutsEngine.run: more iterations than iters_per_call"
-        H.check(H.lib().hmc_nuts_iters(self.T, self.K, self.schedule(it0, it1), self._replay, self.S,
-                                       H.ptr(self.ws), self.stream()), "hmc_nuts_iters")
+        if it1 - it0 > self.iters_per_call:
+            raise ValueError("NutsEngine.run: %d iterations in one call, the workspace is sized for %d "
+                             "(iters_per_call)" % (it1 - it0, self.iters_per_call))
+        # the sized entry checks the workspace against what this call needs (include/hmc.h)
+        H.check(H.lib().hmc_nuts_iters_ws(self.T, self.K, self.schedule(it0, it1), self._replay, self.S,
+                                          H.ptr(self.ws), self.ws.numel() * 8, self.stream()), "hmc_nuts_iters_ws")
