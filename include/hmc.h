@@ -191,8 +191,8 @@ int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max);
  * resample -> E0 -> tree doubling until both ends U-turn (sub-tree U-turn checks against the
  * saved odd points, progressive sampling, biased sub-tree acceptance) -> store.
  * Replaces HMC_sampler.gen_sample_NUTS, samplers.py:563-791 (+ utils.py:222-385).
- * Dense precision only (pass diagonal targets as dense), any D, 1 <= d_max <= 15 (the reference
- * takes any d_max; 15 = 2^15 - 1 leapfrogs per tree, documented in INTEGRATION.md), diagonal or
+ * Dense precision only (pass diagonal targets as dense), any D, 1 <= d_max <= 30 (the reference
+ * takes any d_max; 30 = up to 2^30 - 1 leapfrogs per tree), diagonal or
  * full cov_p (minv_full) at any D:
  *   D <= 128              the 16-chain MFMA tree kernel (hmc_nuts.hip; a full cov_p adds its
  *                         momentum and kinetic products on the same tiles);

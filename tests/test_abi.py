@@ -130,7 +130,8 @@ def test_nuts_workspace_size_query(monkeypatch):
     other = L.hmc_nuts_workspace_size_ex(200, 1000, 10, 8, 0)
     per_chain = L.hmc_nuts_workspace_size_ex(330, 1000, 10, 8, 0) * 200 // 330   # same layout, D-scaled
     assert other >= lock_philox and other >= per_chain * 0.9
-    assert L.hmc_nuts_workspace_size_ex(100, 1000, 16, 8, 1) == 0          # d_max > 15
+    assert L.hmc_nuts_workspace_size_ex(100, 1000, 31, 8, 1) == 0          # d_max > 30
+    assert L.hmc_nuts_workspace_size_ex(100, 1000, 30, 8, 1) > L.hmc_nuts_workspace_size_ex(100, 1000, 15, 8, 1)
     assert L.hmc_nuts_workspace_size_ex(100, 1000, 10, 0, 1) == 0          # iters_per_call < 1
 
 

@@ -98,6 +98,40 @@ def test_diagonal_large_D_vs_oracle(fp_mode):
     _check(eng, ref, Ls)
 
 
+@pytest.mark.parametrize("fp_mode", ["exact", "fast"])
+@pytest.mark.parametrize("D,dense", [(136, True), (2050, False)])
+def test_large_D_chain0_capture_vs_oracle(D, dense, fp_mode):
+    """Chain-0 trajectory capture above the fused kernels' limits (samplers.py:442-475, make_movie's
+    input): phi_q (q[:2] at the start and after every leapfrog step of the first N_save iterations)
+    and decision_chain from the large-D path equal the oracle's on the same replayed draws
+    (this returned HMC_ENOTSUP)."""
+    from hmc_amd.engine import RandomEngine
+    from hmc_amd.target import MVNTarget
+    N, Niter, wu, n_save, dt = 3, 12, 2, 7, 0.08
+    rs = np.random.RandomState(D + 5)
+    cov = O.mvn_cov(D, 0.6) if dense else np.diag(rs.uniform(0.5, 2.0, D))
+    tgt = FastMVN(np.zeros(D), cov)
+    q_start = rs.standard_normal((N, D))
+    p0, P = rs.standard_normal((N, D)), rs.standard_normal((N, Niter, D))
+    Ls = rs.randint(3, 9, size=(N, Niter)).astype(np.int32)
+    lnu = np.log(rs.random_sample((N, Niter)))
+    eng = RandomEngine(MVNTarget(np.zeros(D), cov, logdet_const=tgt.c), N, Niter, wu, 1, 3, 9, dt, rng="replay",
+                       fp_mode=fp_mode, n_save=n_save)
+    eng.set_replay(p0, P, Ls, lnu)
+    eng.init(q_start)
+    eng.run(1, 6)
+    eng.run(6, Niter + 1)
+    ref = O.gen_sample_random(O.HMCCore(tgt, dt), q_start, N, Niter, wu, 1, 3, 9, O.ReplayDraws(p0, P, Ls, lnu),
+                              n_save_chain0=n_save)
+    traj, tl = eng.traj.cpu().numpy(), eng.traj_len.cpu().numpy()
+    np.testing.assert_array_equal(eng.decision.cpu().numpy(), ref["decision_chain"][:n_save])
+    assert len(ref["phi_q"]) == n_save
+    for i, want in enumerate(ref["phi_q"]):
+        assert tl[i] == want.shape[0] == Ls[0, i] + 1
+        np.testing.assert_allclose(traj[i, :tl[i]], want, rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(eng.q_chain.cpu().numpy(), ref["q_chain"], rtol=1e-9, atol=1e-9)
+
+
 @pytest.mark.parametrize("D,rho,dense,full_p", [(160, 0.8, True, False), (2100, 0.0, False, False),
                                                (160, 0.8, True, True)])
 def test_large_D_philox_stationary(D, rho, dense, full_p):

@@ -113,6 +113,33 @@ def test_nuts_deep_tree_single_chain_handoff(fp_mode):
     np.testing.assert_allclose(h.E_chain[:, :, 0], ref["E_chain"], rtol=1e-10, atol=1e-10)
 
 
+def test_nuts_d_max_beyond_15_deep_tree():
+    """d_max above the former bound of 15 (the reference takes any d_max, samplers.py:306,
+    :519-520): one chain, D = 2, dt small enough that a tree needs more than 2^15 points before both
+    ends turn.  Leapfrog counts, q_chain and E equal the oracle's on the same
+    replayed draws, with no d_max hit and no hand-off give-up."""
+    from hmc_amd import _lib as H
+    from hmc_amd.target import MVNTarget
+    D, N, Niter, d_max, dt = 2, 1, 2, 20, 1.2e-4
+    rs = np.random.RandomState(5)
+    q_start = rs.standard_normal((N, D))
+    p0 = rs.standard_normal((N, D))
+    P = rs.standard_normal((N, Niter, D))
+    tape = rs.uniform(0.0, 2.0, (N, Niter * 2 * ((1 << 17) + d_max + 2)))
+    core = O.HMCCore(O.MVNTarget(np.zeros(D), np.eye(D)), dt, None)
+    ref = O.gen_sample_nuts(core, q_start, N, Niter, 0, 1, d_max, O.ReplayDraws(p0, P, tape=tape.copy()),
+                            on_dmax="raise")
+    assert ref["n_leapfrog"] > 1 << 16                 # trees deeper than 15 doublings
+    h = _nuts(D, MVNTarget(np.zeros(D), np.eye(D)), N, Niter, 0, 1, dt, d_max, rng="replay", fp_mode="exact")
+    h.set_nuts_replay(p0, P, tape)
+    h.gen_sample_NUTS(q_start, 0, False)
+    c = h.engine.read_counters()
+    assert c[H.CNT_HANDOFF_GIVEUP] == 0 and c[H.CNT_DMAX] == 0
+    assert h.n_leapfrog == ref["n_leapfrog"]
+    np.testing.assert_allclose(h.q_chain, ref["q_chain"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(h.E_chain[:, :, 0], ref["E_chain"], rtol=1e-10, atol=1e-10)
+
+
 def test_nuts_replay_without_tape_warns():
     """rng='replay' NUTS without set_nuts_replay cannot follow the reference's data-dependent
     np.random order (samplers.py:608, :748, :773): it runs Philox seeded from np.random and says so."""

@@ -164,7 +164,8 @@ def test_nuts_closed_form_save_slots():
     """hmc_nuts.hip keeps saved odd point l of a sub-tree in slot ctz(l - 1) (point 1: slot
     d_max) instead of the reference's searched table (utils.py:222-385): every point that
     check_points(m) names must still be in its slot when m is reached, for every sub-tree size
-    the reference can build (d < d_max <= 15)."""
+    the reference can build (d < d_max <= 15), and for trees up to 2^17 points at d_max = 30 (the
+    kernels' bound: slots depend on d_max only through point 1's)."""
     from hmc_amd.utils import check_points
 
     def slot(l, d_max):
@@ -179,6 +180,14 @@ def test_nuts_closed_form_save_slots():
                 else:
                     for l in check_points(m):
                         assert held.get(slot(int(l), d_max)) == int(l), (d_max, d, m, l)
+    held = {}
+    d_max = 30
+    for m in range(1, (1 << 17) + 1):      # one pass: a tree of 2^17 points holds every smaller one's steps
+        if m % 2:
+            held[slot(m, d_max)] = m
+        elif m & (m - 1) == 0 or m % 64 == 0 or m > (1 << 17) - 4096:
+            for l in check_points(m):
+                assert held.get(slot(int(l), d_max)) == int(l), (d_max, m, l)
 
 
 def test_reference_nuts_drifts_with_a_mass_matrix():

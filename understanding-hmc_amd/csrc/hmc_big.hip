@@ -45,6 +45,14 @@ __device__ __forceinline__ bool write_row_of(const RandArgs& a, int it) {
   return it >= a.wu && ((it == a.niter) || ((it - a.wu + 1) % a.thin == 0));
 }
 
+// chain-0 trajectory capture (samplers.py:442-452, :463-475; make_movie's input): global chain 0
+// in iterations 1 .. n_save writes q[:2] at the start and after every leapfrog step, L + 1 and
+// the Metropolis decision, as the fused kernels do
+__device__ __forceinline__ double* cap_row(const RandArgs& a, uint64_t gc, int it) {
+  return (a.traj_q && gc == 0 && it >= 1 && it <= a.n_save) ? a.traj_q + (int64_t)(it - 1) * a.traj_stride * 2
+                                                           : nullptr;
+}
+
 // ---- iteration start: one wave per chain, lanes over the coordinate pairs
 template <bool DENSE, bool REPLAY, bool MASS = false>
 __global__ __launch_bounds__(256) void k_big_begin(BigArgs b, int it) {
@@ -112,12 +120,17 @@ __global__ __launch_bounds__(256) void k_big_begin(BigArgs b, int it) {
     }
     b.L[c] = L;
     b.lnu[c] = lnu;
+    if (double* cp = cap_row(a, gc, it)) {                        // phi_q_tmp[0] = q[:2] (:444-446)
+      cp[0] = a.q[base];
+      cp[1] = a.q[base + (D > 1 ? 1 : 0)];
+      a.traj_len[it - 1] = (L > 0 ? L : 0) + 1;
+    }
   }
 }
 
 // ---- leapfrog pieces (samplers.py:831-839), elementwise over (chain, dim) for chains with l < L
 template <bool EXACT, bool DENSE, bool DRIFT>
-__global__ __launch_bounds__(256) void k_big_kick(BigArgs b, int l) {
+__global__ __launch_bounds__(256) void k_big_kick(BigArgs b, int l, int it) {
   const RandArgs& a = b.a;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n * (int64_t)a.D) return;
@@ -134,6 +147,8 @@ __global__ __launch_bounds__(256) void k_big_kick(BigArgs b, int l) {
   if constexpr (DRIFT) {
     qd = EXACT ? qd + dt * pd : __builtin_fma(dt, pd, qd);
     a.q[i] = qd;
+    if (d < 2)                                                    // phi_q_tmp[l] = q[:2] (:448-452)
+      if (double* cp = cap_row(a, (uint64_t)(a.chain_offset + c), it)) cp[2 * (l + 1) + d] = qd;
   }
 }
 
@@ -234,6 +249,7 @@ __global__ __launch_bounds__(256) void k_big_end(BigArgs b, int it) {
     }
     if (store) __builtin_nontemporal_store(qd, rowp + d);
   }
+  if (lane == 0 && cap_row(a, (uint64_t)(a.chain_offset + c), it)) a.decision[it - 1] = accept ? 1 : 0;   // :463-466
   if (lane == 0 && a.cnt) {
     unsigned long long* cs = a.cnt + (c & (HMC_COUNTER_SLOTS - 1)) * HMC_NCOUNTERS;
     if (accept) atomicAdd(cs + (post ? HMC_CNT_ACCEPT : HMC_CNT_ACCEPT_WU), 1ull);
@@ -448,10 +464,10 @@ hipError_t big_iterations(const BigArgs& b, bool replay, hipStream_t s) {
       k_big_begin<DENSE, false><<<gw, 256, 0, s>>>(b, it);
     }
     for (int l = 0; l < lmax; ++l) {
-      k_big_kick<EXACT, DENSE, true><<<ge, 256, 0, s>>>(b, l);
+      k_big_kick<EXACT, DENSE, true><<<ge, 256, 0, s>>>(b, l, it);
       if (DENSE)
         if (hipError_t e = grad_all(b, l, s)) return e;
-      k_big_kick<EXACT, DENSE, false><<<ge, 256, 0, s>>>(b, l);
+      k_big_kick<EXACT, DENSE, false><<<ge, 256, 0, s>>>(b, l, it);
     }
     if (mass) {
       if (hipError_t e = gemm_all(b, BigGemm{a.minvf, b.p, false, b.u}, -1, s)) return e;

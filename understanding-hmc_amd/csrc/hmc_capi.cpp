@@ -239,7 +239,6 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
     return fail(HMC_EINVAL, "traj_stride must be >= L_high");
   const bool dense = t->kind == HMC_TARGET_DENSE;
   if (hmc::big_path(dense, t->D)) {   // large D (hmc_big.hip)
-    if (st->n_save > 0 && st->traj_q) return fail(HMC_ENOTSUP, "trajectory capture with D=%d: not supported", t->D);
     if (!st->order) return fail(HMC_EINVAL, "D=%d needs hmc_random_workspace_size() bytes in state.order", t->D);
     const hmc::Layout lay{0, 0, 0, (t->D + 1) / 2};
     hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
@@ -317,7 +316,7 @@ int64_t hmc_random_workspace_size(const hmc_target* t, int64_t n_chains) {
 
 int64_t hmc_nuts_workspace_size_ex(int32_t D, int64_t n_chains, int32_t d_max, int32_t iters_per_call,
                                    int32_t philox_momenta) {
-  if (D < 1 || n_chains < 0 || d_max < 1 || d_max > 15 || iters_per_call < 1) return 0;
+  if (D < 1 || n_chains < 0 || d_max < 1 || d_max > hmc::kNutsDmaxMax || iters_per_call < 1) return 0;
   if (hmc::nuts_lock_path(D)) {   // a full cov_p (philox_momenta 0) takes the per-chain kernel at any D > 128
     const int64_t lock = hmc::nuts_lock_ws_doubles(n_chains, D, d_max);
     return (philox_momenta ? lock : std::max(lock, hmc::nuts_big_ws_doubles(n_chains, D, d_max))) *
@@ -335,7 +334,7 @@ int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max) {
 hmc_status hmc_nuts_iters_ws(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, const hmc_replay* r,
                              hmc_state* st, void* workspace, int64_t workspace_bytes, void* stream) {
   if (hmc_status e = check_schedule(t, k, s, false)) return e;
-  if (s->d_max < 1 || s->d_max > 15) return fail(HMC_EINVAL, "d_max must be in [1, 15]");
+  if (s->d_max < 1 || s->d_max > hmc::kNutsDmaxMax) return fail(HMC_EINVAL, "d_max must be in [1, %d]", hmc::kNutsDmaxMax);
   if (s->iter_end > s->iter_begin && s->n_chains > 0) {
     // the sized workspace must cover this call: its Philox momenta drawn ahead (diagonal cov_p)
     // for this call's iterations, or the tree vectors of the kernel this call takes
@@ -360,7 +359,7 @@ hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_s
     return fail(HMC_EINVAL, "iteration range must satisfy 1 <= begin <= end <= Niter+1");
   if (s->n_chains == 0) return HMC_OK;   // empty batch: zero-size buffers may be NULL
   if (!st->q || !st->E_prev) return fail(HMC_EINVAL, "null state");
-  if (s->d_max < 1 || s->d_max > 15) return fail(HMC_EINVAL, "d_max must be in [1, 15]");
+  if (s->d_max < 1 || s->d_max > hmc::kNutsDmaxMax) return fail(HMC_EINVAL, "d_max must be in [1, %d]", hmc::kNutsDmaxMax);
   if (hmc_status e = check_mass(t, k, s)) return e;
   if (t->kind != HMC_TARGET_DENSE) return fail(HMC_ENOTSUP, "NUTS runs the dense kernel: pass prec as dense");
   const bool big = !hmc::dense_tiles(t->D);   // D > 128: hmc_nuts_big.hip

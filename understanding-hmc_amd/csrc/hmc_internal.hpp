@@ -68,6 +68,9 @@ struct RandArgs {
 // row-major D x D precision.  dense_tiles(D) = 16-dim output tiles per chain (0: unsupported).
 using DenseArgs = RandArgs;
 int dense_tiles(int D);
+// NUTS: the largest d_max the kernels take (samplers.py:306 takes any; a tree of 2^30 - 1 leapfrogs
+// per iteration is far past any practical run; the save slots are d_max + 1 vectors per chain)
+constexpr int kNutsDmaxMax = 30;
 int64_t nuts_ws_doubles(int64_t n, int D, int d_max, int mom_iters);   // mom_iters: Philox momenta drawn ahead
 hipError_t launch_nuts_iters(const RandArgs& a, bool exact, bool replay, hipStream_t s);
 // NUTS for dense D > 128 (hmc_nuts_big.hip): one wave per chain, tree vectors in the workspace.

@@ -247,19 +247,19 @@ __global__ __launch_bounds__(256) void k_nuts_big(RandArgs a, int Dp, int nv) {
         ++n_dmax;
         break;
       }
-      int table[16];                                                           // :601 save-slot table
+      int table[kNutsDmaxMax + 1];                                             // :601 save-slot table
 #pragma unroll
-      for (int s = 0; s < 16; ++s) table[s] = -1;
+      for (int s = 0; s <= kNutsDmaxMax; ++s) table[s] = -1;
       auto find_next = [&]() {                                                 // utils.py:222-228
         int f = -1;
 #pragma unroll
-        for (int s = 15; s >= 0; --s)
+        for (int s = kNutsDmaxMax; s >= 0; --s)
           if (s <= d_max && table[s] == -1) f = s;
         return f;
       };
       auto set_slot = [&](int s, int v) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
+        for (int i = 0; i <= kNutsDmaxMax; ++i)
           if (i == s) table[i] = v;
       };
       auto save = [&](int v) {                                                 // q_save / p_save (:623-626)
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(256) void k_nuts_big(RandArgs a, int Dp, int nv) {
             const int l = cp.pt;
             int s = 0;
 #pragma unroll
-            for (int i = 15; i >= 0; --i)                                      // retrieve_save_index
+            for (int i = kNutsDmaxMax; i >= 0; --i)                            // retrieve_save_index
               if (table[i] == l) s = i;
             const double* q_chk = W.v(kSave0 + 2 * s);
             const double* p_chk = W.v(kSave0 + 2 * s + 1);

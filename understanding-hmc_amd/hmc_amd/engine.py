@@ -311,7 +311,7 @@ class NutsEngine(RandomEngine):
         nbytes = H.lib().hmc_nuts_workspace_size_ex(self.D, self.N, self.d_max, max(1, self.iters_per_call),
                                                     philox_mom)
         if nbytes <= 0:
-            raise NotImplementedError("NUTS kernel: d_max=%d not supported (1 <= d_max <= 15)" % self.d_max)
+            raise NotImplementedError("NUTS kernel: d_max=%d not supported (1 <= d_max <= 30)" % self.d_max)
         self.ws = torch.zeros((nbytes + 7) // 8, dtype=torch.float64, device=self.device)
 
     def set_replay(self, p0, P, tape):
