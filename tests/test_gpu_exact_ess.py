@@ -102,7 +102,7 @@ def test_streaming_exact_matches_oracle_every_dim(D, N, Niter, wu, thin, step, p
     qc = full.q_chain[:, 1:, :].cpu().numpy()
     st = make(False)
     sd = StreamingDiagnostics(N, D, st.L_chain - 1, tmax=16)
-    feed = 200
+    feed = step * (200 // step)
     if per_step:
         for a in range(1, Niter + 1, step):
             st.run_streaming(sd, a, min(a + step, Niter + 1), step, feed=feed)
