@@ -89,12 +89,12 @@ def _engine_pair(D, N, Niter, wu, thin, seed):
     return engine
 
 
-@pytest.mark.parametrize("D,N,Niter,wu,thin,step,per_step", [
-    (1000, 16, 240, 41, 1, 20, True),      # c4's shape ratio: 200 rows, halves of 99 (the bench's calls)
-    (100, 64, 150, 10, 1, 16, False),      # one launch completes a half mid-way
-    (60, 40, 200, 5, 3, 8, False),         # thinned rows
+@pytest.mark.parametrize("D,N,Niter,wu,thin,step,feed,per_step", [
+    (1000, 16, 240, 41, 1, 20, 200, True),  # c4's shape ratio: 200 rows, halves of 99 (the bench's calls)
+    (100, 64, 150, 10, 1, 16, 80, False),   # a window of one half: the second half wraps
+    (60, 40, 200, 5, 3, 8, 200, False),     # thinned rows
 ])
-def test_streaming_exact_matches_oracle_every_dim(D, N, Niter, wu, thin, step, per_step):
+def test_streaming_exact_matches_oracle_every_dim(D, N, Niter, wu, thin, step, feed, per_step):
     from hmc_amd.diagnostics import LAST_INFO, StreamingDiagnostics
     make = _engine_pair(D, N, Niter, wu, thin, seed=D + N)
     full = make(True)
@@ -102,7 +102,7 @@ def test_streaming_exact_matches_oracle_every_dim(D, N, Niter, wu, thin, step, p
     qc = full.q_chain[:, 1:, :].cpu().numpy()
     st = make(False)
     sd = StreamingDiagnostics(N, D, st.L_chain - 1, tmax=16)
-    feed = step * (200 // step)
+    feed = step * (feed // step)
     if per_step:
         for a in range(1, Niter + 1, step):
             st.run_streaming(sd, a, min(a + step, Niter + 1), step, feed=feed)
@@ -110,7 +110,11 @@ def test_streaming_exact_matches_oracle_every_dim(D, N, Niter, wu, thin, step, p
         st.run_streaming(sd, 1, Niter + 1, step, feed=feed)
     assert sd.mode == "exact"
     W = st._stream[1].shape[1]
-    assert W == sd.n + -(-step // thin) + 2                  # one half + a launch's rows
+    # both halves whole when that fits the segment mode's window, else one half + a launch's rows
+    W_seg = 16 + (feed + step) // thin + 2
+    W2 = 2 * sd.n + -(-step // thin) + 2
+    assert W == (W2 if W2 <= W_seg else sd.n + -(-step // thin) + 2)
+    assert (W < W2) == (feed == 80)
     R, neff = sd.finish()
     assert sd.info["truncated_dims"] == 0 and LAST_INFO["mode"] == "streaming-exact"
     assert torch.equal(st.q, full.q)

@@ -1020,6 +1020,8 @@ hipError_t launch_conv_fused(const double* x, int64_t n_chains, int64_t cs, int6
 
 hipError_t launch_half_sums(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int D, int wrap, int slot0,
                             int n, int T, double* work, double* out, hipStream_t st) {
+  // a half that does not reach the window's end reads plain strided rows (no per-row wrap)
+  if (wrap > 0 && slot0 + n <= wrap) wrap = 0;
   Src s{x, cs, ss, 0, n_chains, n, D, 1, wrap, slot0};
   if (wrap <= 0) s.base = (int64_t)slot0 * ss;   // no wrap: sample s in row slot0 + s
   return launch_lags(s, 0, T, 1, 1, 0, T, work, out, st);

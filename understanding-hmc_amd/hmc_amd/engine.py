@@ -168,10 +168,15 @@ class RandomEngine:
         # more window than the segment mode would use: each half is fed once complete, from a
         # window of n + ceil(step/thin) + 2 rows; otherwise segments of `feed` iterations
         exact = diag.mode == "exact" or (diag.mode is None and diag.n <= T + feed // self.thin)
+        W_seg = T + (feed + step) // self.thin + 2
         if exact:
-            W = diag.n + -(-step // self.thin) + 2
+            # both halves whole in the window (rows 1 .. 2n at slots 1 .. 2n: no half wraps, so the
+            # lag pass reads plain strided rows) when that costs no more than the segment mode;
+            # otherwise one half + a launch's rows, the second half wrapping
+            W2 = 2 * diag.n + -(-step // self.thin) + 2
+            W = W2 if W2 <= W_seg else diag.n + -(-step // self.thin) + 2
         else:
-            W = T + (feed + step) // self.thin + 2
+            W = W_seg
         st = getattr(self, "_stream", None)
         if st is not None and st[0] is diag and st[1].shape[1] != W and diag.pos > 0:
             # the window holds the variogram carry (and possibly written but unfed rows) at
