@@ -1,6 +1,8 @@
 """Dev timing of the one-read lag kernel (not a bench line), HIP events per call:
-    python scripts/dev/lag_bench.py half N n D [reps]     hmc_half_sums over one half of a circular
-                                                          window of n + 22 rows (c4: 131072 99 1000)
+    python scripts/dev/lag_bench.py half N n D [reps]     hmc_half_sums over the second half of a window of
+                                                          2n + 22 rows (c4: 131072 99 1000; no wrap, as
+                                                          RandomEngine.run_streaming sizes c4's window)
+    python scripts/dev/lag_bench.py halfwrap N n D [reps] the same over a half that wraps in a window of n + 22
     python scripts/dev/lag_bench.py conv N rows D [reps]  hmc_convergence_sums, every lag (tmax = n - 2)
                                                           of a stored (N, rows, D) window (c3: 262144 400 100;
                                                           headline: 1048576 100 100)
@@ -20,11 +22,11 @@ reps = int(sys.argv[5]) if len(sys.argv) > 5 else 5
 L = H.lib()
 st = torch.cuda.current_stream().cuda_stream
 g = torch.Generator(device="cuda").manual_seed(1)
-if mode == "half":
+if mode in ("half", "halfwrap"):
     n = n_or_rows
-    W = n + 22
+    W = n + 22 if mode == "halfwrap" else 2 * n + 22
     x = torch.randn((N, W, D), dtype=torch.float64, device="cuda", generator=g)
-    slot0 = W - 30                                     # the half wraps after 30 samples
+    slot0 = W - 30 if mode == "halfwrap" else n + 1     # halfwrap: the half wraps after 30 samples
     T = max(1, n - 2)
     series_rows = n
     call = lambda work, out: L.hmc_half_sums(x.data_ptr(), N, x.stride(0), x.stride(1), D, W, slot0, n, T,  # noqa: E731
