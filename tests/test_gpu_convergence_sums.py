@@ -53,6 +53,14 @@ CASES = [
     (5, 115, 70, 0, 1, 1, 55),         # n = 57: one group + the longest tail, 8
     (5, 117, 70, 0, 1, 1, 56),         # n = 58: two groups (a tail of 9 would exceed 8)
     (4, 240, 100, 0, 1, 1, 150),       # tmax beyond n - 1 = 119: the lags past it are 0
+    # complete passes of 128 <= n <= 240 take the matrix cores (k_conv_mfma, Hankel tiles)
+    (3, 257, 13, 0, 1, 1, 126),        # n = 128 (the smallest), D = 13: a partial dim group; 6 split
+                                       # chains: one full chain group of 4 and a ragged one
+    (2, 481, 100, 0, 1, 1, 238),       # n = 240 (the largest): every tile and anchor step
+    (5, 300, 101, 1, 1, 1, 200),       # n = 149, a D = 100 view with odd row stride; tmax beyond n - 1
+    (4, 452, 9, -1, 1, 0, 224),        # storage at an 8-B offset, n = 226, odd D
+    (7, 301, 64, 0, 1, 1, 148),        # n = 150, D = 64: full dim groups
+    (5, 1200, 24, 0, 3, 3, 197),       # thinned view (every 3rd row), n = 199
 ]
 
 
@@ -120,6 +128,27 @@ def test_convergence_stats_n50_vs_oracle(D):
         x[:, t] = -2.0 + rho * (x[:, t - 1] + 2.0) + np.sqrt(1 - rho * rho) * rs.standard_normal((N, D))
     R, neff = G.convergence_stats(x[:, 1:, :], thin_rate=1, warm_up_num=0)
     assert G.LAST_INFO["tmax"] == 48 and G.LAST_INFO["lags"] == 49 and G.LAST_INFO["fallback_dims"] == 0
+    R_ref, neff_ref = O.convergence_stats(x[:, 1:, :], thin_rate=1, warm_up_num=0)
+    np.testing.assert_allclose(R, R_ref, rtol=1e-10)
+    np.testing.assert_allclose(neff, neff_ref, rtol=1e-8)
+
+
+@pytest.mark.parametrize("D", [20, 7])
+def test_convergence_stats_mfma_window_vs_oracle(D):
+    """c3's window shape (split chains of n = 200, every lag 1..199 in one pass on the matrix cores)
+    on slowly to fast mixing AR(1) dims: R-hat and ESS equal the oracle's convergence_stats
+    (utils.py:77-179 restated), no fallback pass."""
+    from hmc_amd import diagnostics as G
+    from oracle import hmc_oracle as O
+    rs = np.random.RandomState(7 + D)
+    N, L = 10, 401
+    rho = np.linspace(0.0, 0.995, D)
+    x = np.empty((N, L, D))
+    x[:, 0] = rs.standard_normal((N, D)) + 1.5
+    for t in range(1, L):
+        x[:, t] = 1.5 + rho * (x[:, t - 1] - 1.5) + np.sqrt(1 - rho * rho) * rs.standard_normal((N, D))
+    R, neff = G.convergence_stats(x[:, 1:, :], thin_rate=1, warm_up_num=0)
+    assert G.LAST_INFO["tmax"] == 198 and G.LAST_INFO["lags"] == 199 and G.LAST_INFO["fallback_passes"] == 0
     R_ref, neff_ref = O.convergence_stats(x[:, 1:, :], thin_rate=1, warm_up_num=0)
     np.testing.assert_allclose(R, R_ref, rtol=1e-10)
     np.testing.assert_allclose(neff, neff_ref, rtol=1e-8)

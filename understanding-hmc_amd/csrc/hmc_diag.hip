@@ -564,6 +564,231 @@ __global__ __launch_bounds__(256) void k_lag_dims(LagArgs a, const double* __res
   out[i] = acc;
 }
 
+// ---- The same one-read sums on the matrix cores (stored complete passes, 128 <= n <= 240: c3's
+// n = 200).  The lag products are GEMM-shaped once the series is laid out as Hankel slices:
+// v_mfma_f64_16x16x4_f64 with A[t'][k] = y_k[b + T + t'] and B[k][s] = y_k[b - s] (k = four split
+// chains of ONE dimension, the contraction index) adds y_k[i] y_k[i + L] to entry (t', s) of tile T,
+// L = T + t' + s, anchor i = b - s.  Tiles T = -16, 0, 16, .. and anchor steps b = 0, 16, ..: a lag
+// L = 16 q + r gets s <= r from tile 16 q and s > r from tile 16 q - 16, so over all b every product
+// y_i y_{i+L} (0 <= i, i + L < n; rows outside [0, n) are zeros in LDS) is added exactly once, and a
+// tile only runs the anchor steps that still meet lags < n (the triangle, at 16-row granularity).
+// V_t = sum_{s>=t} sq_s + sum_{s<=n-1-t} sq_s - 2 C_t with sq_s = sum_j y_{j,s}^2 (no cancellation
+// in the square terms), y = x - x_j[0] per series as in lag_wave.
+// Workgroup = 8 waves = 8 dimensions x a range of split chains; the waves stage each group of four
+// split chains into LDS together (lanes across the 8 dims: 64 B row segments), then each wave runs
+// its dimension's tiles, accumulating across the range in registers (tiles x 4 doubles per lane).
+// Split means and stds come from the same LDS slices (partial sums over rows t' mod 16, reduced in a
+// fixed order: deterministic, within a few ulps of np.mean's sequential sum).
+constexpr int kMfmaNT = 16;                      // tiles T = -16 .. 16 (kMfmaNT - 2)
+constexpr int kMfmaNB = 16;                      // anchor steps b = 0 .. 16 (kMfmaNB - 1)
+constexpr int kMfmaMaxN = 16 * (kMfmaNT - 1);    // 240 samples per split chain
+constexpr int kMfmaMinN = 128;
+constexpr int kMfmaRows = (kMfmaMaxN + 15) / 16; // staged rows per thread (16-row phases)
+constexpr int kMfmaDims = 8;                     // dimensions (waves) per workgroup
+constexpr int kMfmaPW = kMfmaNT * 256 + 256 + 4; // partial doubles per wave: tiles, sq rows, moments
+
+struct MfmaArgs {
+  Src s;
+  int P;            // LDS doubles per series (rows -16 .. n + 29, stride = 16 mod 32)
+  int NT, NB;       // tiles and anchor steps used
+  int G;            // dimension groups ceil(D / 8)
+  int R;            // split-chain ranges (a multiple of 8)
+  int64_t per;      // split chains per range (a multiple of 4)
+};
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_mfma(MfmaArgs a,
+                                                                                             double* partial) {
+  extern __shared__ double lds[];                 // [8 dims][4 chains][P] samples, then x0[32]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  // XCD-major: the G dimension groups of one chain range run on one XCD (blocks id, id + 8, ..
+  // share an XCD), so a row's 64-B segments are fetched into that L2 once
+  const int id = blockIdx.x;
+  const int local = id >> 3;
+  const int r = (local / a.G) * 8 + (id & 7), g = local % a.G;
+  const Src& s = a.s;
+  const int n = s.n, D = s.D, P = a.P;
+  const int64_t m2 = n_series(s);
+  const int64_t jlo = (int64_t)r * a.per;
+  const int64_t jhi = jlo + a.per < m2 ? jlo + a.per : m2;
+  double* const x0l = lds + 32 * P;
+  for (int i = tid; i < 32 * P + 32 + 320; i += 512) lds[i] = 0.0;
+  // staging role: thread = (dim w, chain k of the group, row phase rho); rows rho + 16 i
+  const int sw = tid & 7, sk = (tid >> 3) & 3, rho = tid >> 5;
+  const int sd = g * kMfmaDims + sw;
+  double xs[kMfmaRows];
+  double x0s = 0.0;
+  auto stage_load = [&](int64_t jg) {
+    const int64_t j = jg + sk;
+    const bool ok = sd < D && j < jhi;
+    x0s = ok ? split_ptr(s, j, 0)[sd] : 0.0;
+#pragma unroll
+    for (int i = 0; i < kMfmaRows; ++i) {
+      const int row = rho + 16 * i;
+      xs[i] = (ok && row < n) ? split_ptr(s, j, row)[sd] : x0s;
+    }
+  };
+  auto stage_store = [&]() {
+    double* dst = lds + (sw * 4 + sk) * P + 16;
+#pragma unroll
+    for (int i = 0; i < kMfmaRows; ++i) {
+      const int row = rho + 16 * i;
+      if (row < n) dst[row] = xs[i] - x0s;     // rows >= n stay zero
+    }
+    if (rho == 0) x0l[sw * 4 + sk] = x0s;
+  };
+  // consumer role: wave wv = dimension d; lane = (chain k = lane >> 4, t' or s = lane & 15)
+  const int d = g * kMfmaDims + wv;
+  const int k = lane >> 4, c16 = lane & 15;
+  const double* const ser = lds + (wv * 4 + k) * P + 16;
+  const double Sd = d < D ? s.x[s.base + d] : 0.0;
+  typedef double v4d __attribute__((ext_vector_type(4)));
+  v4d acc[kMfmaNT];
+#pragma unroll
+  for (int t = 0; t < kMfmaNT; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+  double sqm[kMfmaRows];
+#pragma unroll
+  for (int i = 0; i < kMfmaRows; ++i) sqm[i] = 0.0;
+  double a_std = 0.0, a_m = 0.0, a_m2 = 0.0;
+  const int NT = a.NT;
+  const double dn = n;
+  int64_t jg = jlo;
+  if (jg < jhi) stage_load(jg);
+  for (; jg < jhi; jg += 4) {
+#ifndef HMC_MFMA_DEV_NOSTAGE                      // dev timing variant: matrix work on stale LDS
+    __syncthreads();                              // the previous group's slices are read
+    stage_store();
+    __syncthreads();
+    if (jg + 4 < jhi) stage_load(jg + 4);         // in flight under this group's matrix work
+#endif
+    if (d < D) {
+      double ps1 = 0.0, ps2 = 0.0;
+      // the step bounds are recomputed per group from an opaque copy of n: hoisted out of the
+      // group loop, the 256 tile tests were live scalar masks (spilled)
+      int nn = n;
+      asm volatile("" : "+s"(nn));
+      // software-pipelined: the next tile's A slice and the next step's B slice are read one MFMA
+      // ahead (unconditionally up to the largest tile any n <= kMfmaMaxN runs at this step; the LDS
+      // carries slack past the last series for those reads)
+      double bn = ser[-c16];                      // B of step 0
+      auto bstep = [&](auto bi_c) {
+        constexpr int bi = decltype(bi_c)::value;
+        constexpr int TLS = (kMfmaMaxN + 14 - 16 * bi) / 16 + 1 < kMfmaNT - 1 ? (kMfmaMaxN + 14 - 16 * bi) / 16 + 1
+                                                                                 : kMfmaNT - 1;
+        if (16 * bi <= nn + 14) {
+          // last tile whose lags (>= T) still meet an anchor >= 16 bi - 15: 16 (ti - 1) <= n + 14 - 16 bi
+          const int tl = min(NT - 1, (nn + 14 - 16 * bi) / 16 + 1);
+          const double bv = bn;
+          if constexpr (bi + 1 < kMfmaNB) bn = ser[16 * (bi + 1) - c16];
+          double an = ser[16 * bi - 16 + c16];    // tile 0 (T = -16)
+          auto tile = [&](auto ti_c) {
+            constexpr int ti = decltype(ti_c)::value;
+            if constexpr (ti <= TLS) {
+              const double av = an;
+              if constexpr (ti + 1 <= TLS) an = ser[16 * bi + 16 * ti + c16];
+              if (ti <= tl) {
+                if constexpr (ti == 1 && bi < kMfmaRows) {   // T = 0: rows 16 bi + t' (moments, sq)
+                  const double a2 = av * av;
+                  ps1 += av;
+                  ps2 += a2;
+                  sqm[bi] += a2;
+                }
+#ifdef HMC_MFMA_DEV_NOLDS                         // dev timing variant: no LDS operands
+                acc[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(dn, dn, acc[ti], 0, 0, 0);
+#else
+                acc[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[ti], 0, 0, 0);
+#endif
+              }
+            }
+          };
+          static_for<kMfmaNT>(tile);
+        }
+      };
+      static_for<kMfmaNB>(bstep);
+      // split moments of chain k: reduce the 16 row phases (fixed xor order)
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) {
+        ps1 += __shfl_xor(ps1, m, 64);
+        ps2 += __shfl_xor(ps2, m, 64);
+      }
+      if (jg + k < jhi) {
+        const double mm2 = ps2 - ps1 * ps1 / dn;
+        a_std += sqrt(mm2 > 0.0 ? mm2 / (dn - 1.0) : 0.0);
+        const double e = (x0l[wv * 4 + k] - Sd) + ps1 / dn;
+        a_m += e;
+        a_m2 = __builtin_fma(e, e, a_m2);
+      }
+    }
+  }
+  // partial of this wave: tiles (entry t' * 16 + s), sq rows (summed over the 4 chain lanes), moments
+  double* out = partial + ((int64_t)id * kMfmaDims + wv) * kMfmaPW;
+#pragma unroll
+  for (int t = 0; t < kMfmaNT; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[t * 256 + q * 64 + lane] = acc[t][q];
+#pragma unroll
+  for (int i = 0; i < kMfmaRows; ++i) {
+    double v = sqm[i];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (lane < 16) out[kMfmaNT * 256 + 16 * i + lane] = v;
+  }
+  a_std += __shfl_xor(a_std, 16, 64);
+  a_std += __shfl_xor(a_std, 32, 64);
+  a_m += __shfl_xor(a_m, 16, 64);
+  a_m += __shfl_xor(a_m, 32, 64);
+  a_m2 += __shfl_xor(a_m2, 16, 64);
+  a_m2 += __shfl_xor(a_m2, 32, 64);
+  if (lane == 0) {
+    out[kMfmaNT * 256 + 256] = a_std;
+    out[kMfmaNT * 256 + 257] = a_m;
+    out[kMfmaNT * 256 + 258] = a_m2;
+  }
+}
+
+// red[d][e] = sum over the chain ranges (in order) of the partial entry e of dimension d's wave
+__global__ __launch_bounds__(256) void k_mfma_ranges(MfmaArgs a, const double* __restrict__ partial,
+                                                     double* __restrict__ red) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)a.s.D * kMfmaPW) return;
+  const int d = (int)(i / kMfmaPW), e = (int)(i - (int64_t)d * kMfmaPW);
+  const int g = d / kMfmaDims, w = d - g * kMfmaDims;
+  double acc = 0.0;
+  for (int r = 0; r < a.R; ++r) {
+    const int id = ((r >> 3) * a.G + g) * 8 + (r & 7);   // inverse of k_conv_mfma's block map
+    acc += partial[((int64_t)id * kMfmaDims + w) * kMfmaPW + e];
+  }
+  red[i] = acc;
+}
+
+// out in the conv layout of k_lag_dims (std, mean - S, (mean - S)^2, lags 1 .. nlag, lag n - 1)
+__global__ __launch_bounds__(256) void k_mfma_dims(MfmaArgs a, const double* __restrict__ red, int nlag,
+                                                   double* __restrict__ out) {
+  const int D = a.s.D, n = a.s.n;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)(nlag + 4) * D) return;
+  const int orow = (int)(i / D), d = (int)(i - (int64_t)orow * D);
+  const double* rd = red + (int64_t)d * kMfmaPW;
+  const double* sq = rd + kMfmaNT * 256;
+  if (orow < 3) {
+    out[i] = sq[256 + orow];
+    return;
+  }
+  const int t = orow == nlag + 3 ? n - 1 : orow - 2;
+  double v = 0.0;
+  if (t >= 1 && t < n) {
+    const int q = t >> 4, rr = t & 15;
+    double c = 0.0;                               // C_t: tile 16 q (s <= r), tile 16 q - 16 (s > r)
+    for (int sc = 0; sc <= rr; ++sc) c += rd[(q + 1) * 256 + (rr - sc) * 16 + sc];
+    for (int sc = rr + 1; sc < 16; ++sc) c += rd[q * 256 + (rr + 16 - sc) * 16 + sc];
+    double suf = 0.0, pre = 0.0;
+    for (int r2 = t; r2 < n; ++r2) suf += sq[r2];
+    for (int r2 = 0; r2 <= n - 1 - t; ++r2) pre += sq[r2];
+    v = (suf + pre) - 2.0 * c;
+  }
+  out[i] = v;
+}
+
 // ---- streaming (windowed) split-chain statistics: q_chain never has to be stored whole.
 // Sample position p (0-based over q_chain[:, 1:, :]) lies in split half h = p / n at offset
 // s = p - h*n (positions >= 2n are not part of any split chain, utils.py:102-104).  A call
@@ -885,6 +1110,64 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T <= 16 ? 3
 
 int64_t rows_chunks(int64_t rows) { return (rows + kRowChunk - 1) / kRowChunk; }
 
+// The matrix-core pass's geometry: ranges R (a multiple of 8) picked so that R x G workgroups (one
+// per CU at a time) end in as full a last round as possible, at least 4 rounds.
+MfmaArgs mfma_args(const Src& s) {
+  MfmaArgs a{};
+  a.s = s;
+  const int n = s.n;
+  a.P = 32 * ((n + 46 - 16 + 31) / 32) + 16;
+  a.NT = (n - 1) / 16 + 2;
+  a.NB = (n + 14) / 16 + 1;
+  a.G = (s.D + kMfmaDims - 1) / kMfmaDims;
+  const int64_t m2 = n_series(s);
+  const int64_t groups = (m2 + 3) / 4;
+  const int cus = device_cus();
+  int best = 8;
+  double best_eff = -1.0;
+  for (int x = 1; x <= 64; ++x) {
+    const int64_t R = 8 * x;
+    if (R > groups) break;
+    const int64_t wgs = R * a.G;
+    const int64_t rounds = (wgs + cus - 1) / cus;
+    double eff = (double)wgs / (double)(rounds * cus);
+    if (rounds < 4) eff *= 0.5;                   // too few workgroups per CU to balance
+    if (eff > best_eff + 1e-9) {
+      best_eff = eff;
+      best = (int)R;
+    }
+  }
+  a.R = best;
+  a.per = ((groups + a.R - 1) / a.R) * 4;
+  return a;
+}
+
+bool mfma_ok(const Src& s, int T) {
+  return s.halves == 2 && s.wrap == 0 && s.n >= kMfmaMinN && s.n <= kMfmaMaxN && T >= s.n - 2 &&
+         n_series(s) >= 4;
+}
+
+// samples, x0, and slack for the pipelined reads past the last series (rows up to 16 + 285)
+size_t mfma_lds(const MfmaArgs& a) { return (size_t)(32 * a.P + 32 + 320) * sizeof(double); }
+
+int64_t mfma_work(const MfmaArgs& a) {
+  return (int64_t)a.R * a.G * kMfmaDims * kMfmaPW + (int64_t)a.s.D * kMfmaPW;
+}
+
+hipError_t launch_conv_mfma(const Src& s, int nlag, double* work, double* out, hipStream_t st) {
+  const MfmaArgs a = mfma_args(s);
+  double* partial = work;
+  double* red = work + (int64_t)a.R * a.G * kMfmaDims * kMfmaPW;
+  k_conv_mfma<<<(unsigned)(a.R * a.G), 512, mfma_lds(a), st>>>(a, partial);
+  if (hipError_t e = hipGetLastError()) return e;
+  const int64_t nr = (int64_t)s.D * kMfmaPW;
+  k_mfma_ranges<<<(unsigned)((nr + 255) / 256), 256, 0, st>>>(a, partial, red);
+  if (hipError_t e = hipGetLastError()) return e;
+  const int64_t no = (int64_t)(nlag + 4) * s.D;
+  k_mfma_dims<<<(unsigned)((no + 255) / 256), 256, 0, st>>>(a, red, nlag, out);
+  return hipGetLastError();
+}
+
 // G lag groups (and the tail) of a pass over lags L0 + 1 .. L0 + T.  A first pass (mom) asking for
 // every lag (T >= n - 2; lag n - 1 always comes from the tail) runs the groups up to lag
 // n - 1 - tail only and sums the rest, tail <= kLagTail lags, in difference form.
@@ -1010,11 +1293,23 @@ hipError_t launch_rowsum(const double* x, int64_t n_outer, int64_t os, int64_t n
   return hipGetLastError();
 }
 
-int64_t diag_conv_work(int64_t n_chains, int D, int T) { return lag_work_bound(n_chains, D, T, 1); }
+int64_t diag_conv_work(int64_t n_chains, int D, int T) {
+  int64_t w = lag_work_bound(n_chains, D, T, 1);
+  // a complete pass of split chains of kMfmaMinN .. T + 2 samples may take the matrix cores (their
+  // geometry depends on the chains and dims only)
+  if (T + 2 >= kMfmaMinN) {
+    Src s{nullptr, 0, 0, 0, n_chains, kMfmaMinN, D};
+    w = std::max(w, mfma_work(mfma_args(s)));
+  }
+  return w;
+}
 
 hipError_t launch_conv_fused(const double* x, int64_t n_chains, int64_t cs, int64_t ss, int64_t base, int n, int D,
                              int T, double* work, double* out, hipStream_t st) {
   Src s{x, cs, ss, base, n_chains, n, D};
+#ifndef HMC_LAG_NO_MFMA
+  if (mfma_ok(s, T)) return launch_conv_mfma(s, T, work, out, st);
+#endif
   return launch_lags(s, 0, T, 1, 1, 0, T, work, out, st);
 }
 

@@ -51,6 +51,7 @@ struct RandArgs {
   int Lq, q_row0;        // q_chain buffer: rows per chain (row r at r % Lq) and the first row stored
   int d_max, on_dmax;    // NUTS (hmc_nuts.hip)
   unsigned wait_cap;     // NUTS: wave steps a slot waits for a chain hand-off before giving up
+  int nuts_kb;           // NUTS: iterations of the launch's chain-affine block units (0: tree units only)
   double* ws;            // NUTS per-chain workspace (vectors: live points, boundaries, save slots)
   const double* tape;    // NUTS replay tape [n][tape_stride] (directions / uniforms in consumption order)
   int64_t tape_stride;

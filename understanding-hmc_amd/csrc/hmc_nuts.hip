@@ -34,6 +34,21 @@ namespace {
 #endif
 constexpr int kNutsWaves = HMC_NUTS_WAVES;
 
+// Chain affinity (work queue below): a launch's first K - kNutsTail iterations of every chain run in
+// units of kNutsBlock consecutive iterations (a slot keeps its chain from tree to tree inside a unit:
+// no write-back, drain, publish, poll or state loads between them), queued block-major so a chain's
+// next block waits behind the whole grid's current one; its last kNutsTail iterations run as one unit
+// per (chain, iteration), which keeps the launch's tail at one tree per slot.  kNutsBlock 1 gives the
+// per-tree units only.
+#ifndef HMC_NUTS_BLOCK
+#define HMC_NUTS_BLOCK 8
+#endif
+#ifndef HMC_NUTS_TAIL
+#define HMC_NUTS_TAIL 4
+#endif
+constexpr int kNutsBlock = HMC_NUTS_BLOCK;
+constexpr int kNutsTail = HMC_NUTS_TAIL;
+
 // S_FETCH: the chain slot hands its chain back and takes the next (chain, iteration) unit of the
 // launch from the queue (or retires); S_WAIT: the unit's chain is still finishing its previous
 // iteration in another slot; S_GRAD: a fetched chain waits one wave step for the MFMA gradient at
@@ -74,9 +89,11 @@ __device__ __forceinline__ double ld_wt_d(const double* p) {
 // the factor 4 covers the difference.  A holder can still be slowed far more than that (clock or
 // XCD variation, several ranks sharing one GPU), so the cap never drops below 2^20 wave steps: a
 // give-up is a hard error and only a broken hand-off may trip it.
-inline unsigned nuts_wait_cap(int64_t slots, int64_t n, int d_max) {
+inline unsigned nuts_wait_cap(int64_t slots, int64_t n, int d_max, int kb) {
   const int64_t inflight = (slots + n - 1) / std::max<int64_t>(n, 1) + 1;
-  const int64_t cap = std::max<int64_t>(4 * inflight * ((int64_t(1) << (d_max + 1)) + 64), int64_t(1) << 20);
+  // a block unit holds its chain for kb trees (wait: the chain's previous unit)
+  const int64_t trees = std::max(kb, 1);
+  const int64_t cap = std::max<int64_t>(4 * inflight * trees * ((int64_t(1) << (d_max + 1)) + 64), int64_t(1) << 20);
   return (unsigned)std::min<int64_t>(cap, 0x7FFFFFFF);
 }
 
@@ -340,8 +357,11 @@ void k_nuts_iters(RandArgs a) {
   unsigned long long* const queue = reinterpret_cast<unsigned long long*>(tcur + n_waves * 16);   // zeroed per launch
   unsigned* const done = reinterpret_cast<unsigned*>(queue + 2);    // per chain: iterations done (zeroed per launch)
   const double* const pm = reinterpret_cast<const double*>(queue) + nuts_queue_bytes(a.n) / 8;   // k_nuts_momenta
-  const unsigned long long n_units = (unsigned long long)a.n * (unsigned long long)(a.it1 - a.it0);
+  const int n_blk = (a.nuts_kb + kNutsBlock - 1) / kNutsBlock;   // block units per chain
+  const unsigned long long nb = (unsigned long long)a.n * (unsigned long long)n_blk;
+  const unsigned long long n_units = nb + (unsigned long long)a.n * (unsigned long long)(a.it1 - a.it0 - a.nuts_kb);
   unsigned waited = 0;
+  int it_last = 0;                                      // the current unit's last iteration
   int64_t c = 0;
   bool live = false;
   uint64_t gc = 0;
@@ -402,7 +422,21 @@ void k_nuts_iters(RandArgs a) {
             if (h + 4 * m < a.D) rowp[h + 4 * m] = q[m];
         }
         Eprev = E_init;
-        state = S_FETCH;                                // hand the chain back after each tree
+        if (it < it_last) {                             // a block unit: the same chain's next tree,
+          ++it;                                         // no hand-off (q, E_prev and the tape cursor
+          if constexpr (PG) {                           // stay in registers), its momentum loaded
+            const double* pv = pm + (c * (a.it1 - a.it0) + (it - a.it0)) * (4 * M) + 2 * h;
+#pragma unroll
+            for (int m = 0; m < ME; m += 2) {
+              const double2 z = *reinterpret_cast<const double2*>(pv + 4 * m);
+              p[m] = z.x;
+              p[m + 1] = z.y;
+            }
+          }
+          state = S_GRAD;                               // gradient at q in the next wave step
+        } else {
+          state = S_FETCH;                              // hand the chain back after its unit
+        }
       }
       NUTS_SUBPHASE(8);
       if (state == S_FETCH && live) {                   // tree done: write the chain's state through
@@ -417,9 +451,11 @@ void k_nuts_iters(RandArgs a) {
       if (__builtin_amdgcn_ballot_w64(state == S_FETCH && live)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the state has reached L2/memory ...
 #ifdef HMC_NUTS_RELACQ
-        // A/B variant: the HIP memory model's own agent-scope release/acquire pair
+        // A/B variant on the HIP memory model: one agent-scope release fence per wave step that
+        // publishes (an L2 write-back across XCDs), then relaxed atomic publishes
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         if (state == S_FETCH && live && h == 0)
-          __hip_atomic_store(done + c, (unsigned)(it + 1 - a.it0), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(done + c, (unsigned)(it + 1 - a.it0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
         if (state == S_FETCH && live && h == 0) st_wt(done + c, (unsigned)(it + 1 - a.it0));   // ... then publish
 #endif
@@ -432,8 +468,20 @@ void k_nuts_iters(RandArgs a) {
         u = __shfl(u, lane & 15, kWave);
         if (fetching) {
           if (u < n_units) {
-            c = (int64_t)(u % (unsigned long long)a.n);
-            it = a.it0 + (int)(u / (unsigned long long)a.n);
+            // units 0 .. nb-1: block b = u / n of chain u % n, kNutsBlock iterations run back to
+            // back by this slot (chain affinity); then one unit per (chain, iteration) of the
+            // launch's last iterations, iteration-major, so the launch's tail is one tree per slot
+            if (u < nb) {
+              const int b = (int)(u / (unsigned long long)a.n);
+              c = (int64_t)(u % (unsigned long long)a.n);
+              it = a.it0 + b * kNutsBlock;
+              it_last = a.it0 + min((b + 1) * kNutsBlock, a.nuts_kb) - 1;
+            } else {
+              const unsigned long long ut = u - nb;
+              c = (int64_t)(ut % (unsigned long long)a.n);
+              it = a.it0 + a.nuts_kb + (int)(ut / (unsigned long long)a.n);
+              it_last = it;
+            }
             gc = (uint64_t)(a.chain_offset + c);
             waited = 0;
             state = S_WAIT;
@@ -448,7 +496,9 @@ void k_nuts_iters(RandArgs a) {
         bool ready = need == 0;
         if (!ready) {
 #ifdef HMC_NUTS_RELACQ
-          ready = __hip_atomic_load(done + c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= need;
+          // relaxed polls; the acquire fence (an L2 invalidate) once, in the step a poll succeeds
+          ready = __hip_atomic_load(done + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need;
+          if (__builtin_amdgcn_ballot_w64(ready)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #else
           ready = ld_wt(done + c) >= need;
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the state loads below the poll
@@ -898,7 +948,9 @@ hipError_t launch_nuts_mt3(const RandArgs& args, bool gen, bool replay, hipStrea
   const int64_t wave_doubles = (int64_t)(V_SLOTS + 2 * (a.d_max + 1)) * 4 * MT * kWave;
   double* queue = a.ws + n_waves * wave_doubles + n_waves * 16;   // queue head, (unused), done[n]
   if (hipError_t e = hipMemsetAsync(queue, 0, nuts_queue_bytes(a.n), s)) return e;
-  a.wait_cap = nuts_wait_cap((int64_t)grid.x * kNutsWaves * 16, a.n, a.d_max);
+  // chain affinity: all but the launch's last kNutsTail iterations run in kNutsBlock-tree units
+  a.nuts_kb = kNutsBlock > 1 ? std::max(0, (a.it1 - a.it0) - kNutsTail) : 0;
+  a.wait_cap = nuts_wait_cap((int64_t)grid.x * kNutsWaves * 16, a.n, a.d_max, std::min(a.nuts_kb, kNutsBlock));
   const size_t lds = (size_t)MT * 4 * MT * kWave * sizeof(double);
 #ifdef HMC_NUTS_DEV_C5
   if constexpr (MT == 7 && !EXACT) k_nuts_iters<MT, EXACT, false, false, false, kShortAlways><<<grid, 64 * kNutsWaves, lds, s>>>(a);
