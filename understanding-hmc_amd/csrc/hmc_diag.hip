@@ -564,7 +564,7 @@ __global__ __launch_bounds__(256) void k_lag_dims(LagArgs a, const double* __res
   out[i] = acc;
 }
 
-// ---- The same one-read sums on the matrix cores (stored complete passes, 128 <= n <= 240: c3's
+// ---- The same one-read sums on the matrix cores (stored complete passes, 128 <= n <= 208: c3's
 // n = 200).  The lag products are GEMM-shaped once the series is laid out as Hankel slices:
 // v_mfma_f64_16x16x4_f64 with A[t'][k] = y_k[b + T + t'] and B[k][s] = y_k[b - s] (k = four split
 // chains of ONE dimension, the contraction index) adds y_k[i] y_k[i + L] to entry (t', s) of tile T,
@@ -574,138 +574,162 @@ __global__ __launch_bounds__(256) void k_lag_dims(LagArgs a, const double* __res
 // tile only runs the anchor steps that still meet lags < n (the triangle, at 16-row granularity).
 // V_t = sum_{s>=t} sq_s + sum_{s<=n-1-t} sq_s - 2 C_t with sq_s = sum_j y_{j,s}^2 (no cancellation
 // in the square terms), y = x - x_j[0] per series as in lag_wave.
-// Workgroup = 8 waves = 8 dimensions x a range of split chains; the waves stage each group of four
-// split chains into LDS together (lanes across the 8 dims: 64 B row segments), then each wave runs
-// its dimension's tiles, accumulating across the range in registers (tiles x 4 doubles per lane).
-// Split means and stds come from the same LDS slices (partial sums over rows t' mod 16, reduced in a
-// fixed order: deterministic, within a few ulps of np.mean's sequential sum).
+// Workgroup = 4 waves = 4 dimensions x a range of split chains (two workgroups per CU, so one's
+// staging runs beside the other's matrix work): the waves stage each group of four split chains
+// into LDS together (lanes across the 4 dims: 32-B row segments; each row's other segments are read
+// by the neighbouring dimension groups on the same XCD), then each wave runs its dimension's tiles,
+// accumulating across the range in registers (tiles x 4 doubles per lane).  Split means and stds come
+// from the same A slices (partial sums over rows t' mod 16, reduced in a fixed order: deterministic,
+// within a few ulps of np.mean's sequential sum).
 constexpr int kMfmaNT = 16;                      // tiles T = -16 .. 16 (kMfmaNT - 2)
-constexpr int kMfmaNB = 16;                      // anchor steps b = 0 .. 16 (kMfmaNB - 1)
-constexpr int kMfmaMaxN = 16 * (kMfmaNT - 1);    // 240 samples per split chain
+constexpr int kMfmaMaxN = 16 * (kMfmaNT - 3);    // 208 samples per split chain (NTM = 14)
 constexpr int kMfmaMinN = 128;
-constexpr int kMfmaRows = (kMfmaMaxN + 15) / 16; // staged rows per thread (16-row phases)
-constexpr int kMfmaDims = 8;                     // dimensions (waves) per workgroup
+constexpr int kMfmaDims = 4;                     // waves (dimensions) per workgroup
+constexpr int kMfmaThreads = 64 * kMfmaDims;
+constexpr int kMfmaSer = 4 * kMfmaDims;          // series staged per chain group
+constexpr int kMfmaSlack = 320;                  // doubles past the last series (read-ahead)
 constexpr int kMfmaPW = kMfmaNT * 256 + 256 + 4; // partial doubles per wave: tiles, sq rows, moments
 
 struct MfmaArgs {
   Src s;
   int P;            // LDS doubles per series (rows -16 .. n + 29, stride = 16 mod 32)
   int NT, NB;       // tiles and anchor steps used
-  int G;            // dimension groups ceil(D / 8)
+  int G;            // dimension groups ceil(D / kMfmaDims)
   int R;            // split-chain ranges (a multiple of 8)
   int64_t per;      // split chains per range (a multiple of 4)
 };
 
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_mfma(MfmaArgs a,
+template <int NTM>
+__global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_mfma(MfmaArgs a,
                                                                                              double* partial) {
-  extern __shared__ double lds[];                 // [8 dims][4 chains][P] samples, then x0[32]
+  // capacity of this instance: NTM tiles, NTM - 1 anchor steps, n <= 16 (NTM - 1)
+  constexpr int kNB = NTM - 1, kRows = NTM - 1;
+  // LDS: [dims][4 chains][P] samples, x0[16], slack, sq rows [dims][4 chain lanes][256]
+  extern __shared__ double lds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   // XCD-major: the G dimension groups of one chain range run on one XCD (blocks id, id + 8, ..
-  // share an XCD), so a row's 64-B segments are fetched into that L2 once
+  // share an XCD), so a row's segments are fetched into that L2 once
   const int id = blockIdx.x;
   const int local = id >> 3;
   const int r = (local / a.G) * 8 + (id & 7), g = local % a.G;
   const Src& s = a.s;
   const int n = s.n, D = s.D, P = a.P;
+  const int SB = kMfmaSer * P;
+  double* const x0l = lds + SB;
+  double* const sqb = x0l + kMfmaSer + kMfmaSlack;
   const int64_t m2 = n_series(s);
   const int64_t jlo = (int64_t)r * a.per;
   const int64_t jhi = jlo + a.per < m2 ? jlo + a.per : m2;
-  double* const x0l = lds + 32 * P;
-  for (int i = tid; i < 32 * P + 32 + 320; i += 512) lds[i] = 0.0;
-  // staging role: thread = (dim w, chain k of the group, row phase rho); rows rho + 16 i
-  const int sw = tid & 7, sk = (tid >> 3) & 3, rho = tid >> 5;
+  for (int i = tid; i < SB + kMfmaSer + kMfmaSlack + kMfmaSer * 256; i += kMfmaThreads) lds[i] = 0.0;
+  // staging role: thread = (dim sw, chain sk of the group, row phase rho); rows rho + 16 i
+  const int sw = tid % kMfmaDims, sk = (tid / kMfmaDims) & 3, rho = tid / (4 * kMfmaDims);
   const int sd = g * kMfmaDims + sw;
-  double xs[kMfmaRows];
+  double xs[kRows];
   double x0s = 0.0;
+  bool sok = false;
+  // buffer loads based at the group's first split chain (uniform): one 32-bit lane offset (host-
+  // checked below kLagOOB; lanes past the range or the dims read zeros), rows clamped to n - 1 and
+  // recomputed per group (hoisted, 13 row addresses stayed live through the matrix loop)
+  const int rowb = (int)(s.sample_stride * 8);
   auto stage_load = [&](int64_t jg) {
     const int64_t j = jg + sk;
-    const bool ok = sd < D && j < jhi;
-    x0s = ok ? split_ptr(s, j, 0)[sd] : 0.0;
+    sok = sd < D && j < jhi;
+    const double* b = uni(split_ptr(s, jg, 0));
+    const int lo = sok ? (int)((split_ptr(s, j, 0) - b) + sd) * 8 : kLagOOB + 64;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(b), 0, kLagOOB, 0x00020000);
+    int ro = rho;
+    asm volatile("" : "+v"(ro));
+    x0s = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lo, 0, 0));
 #pragma unroll
-    for (int i = 0; i < kMfmaRows; ++i) {
-      const int row = rho + 16 * i;
-      xs[i] = (ok && row < n) ? split_ptr(s, j, row)[sd] : x0s;
+    for (int i = 0; i < kRows; ++i) {
+      const int row = min(ro + 16 * i, n - 1);
+      xs[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lo + row * rowb, 0, 0));
     }
   };
-  auto stage_store = [&]() {
+  auto stage_store = [&](int nn) {
     double* dst = lds + (sw * 4 + sk) * P + 16;
 #pragma unroll
-    for (int i = 0; i < kMfmaRows; ++i) {
+    for (int i = 0; i < kRows; ++i) {
       const int row = rho + 16 * i;
-      if (row < n) dst[row] = xs[i] - x0s;     // rows >= n stay zero
+      if (row < nn) dst[row] = sok ? xs[i] - x0s : 0.0;   // rows >= n stay zero
     }
-    if (rho == 0) x0l[sw * 4 + sk] = x0s;
+    if (rho == 0) x0l[sw * 4 + sk] = sok ? x0s : 0.0;
   };
-  // consumer role: wave wv = dimension d; lane = (chain k = lane >> 4, t' or s = lane & 15)
+  // matrix role: wave wv = dimension d; lane = (chain k = lane >> 4, t' or s = lane & 15)
   const int d = g * kMfmaDims + wv;
   const int k = lane >> 4, c16 = lane & 15;
-  const double* const ser = lds + (wv * 4 + k) * P + 16;
   const double Sd = d < D ? s.x[s.base + d] : 0.0;
   typedef double v4d __attribute__((ext_vector_type(4)));
-  v4d acc[kMfmaNT];
+  v4d acc[NTM];
 #pragma unroll
-  for (int t = 0; t < kMfmaNT; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
-  double sqm[kMfmaRows];
-#pragma unroll
-  for (int i = 0; i < kMfmaRows; ++i) sqm[i] = 0.0;
+  for (int t = 0; t < NTM; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+  double* const sqa = sqb + (wv * 4 + k) * 256;   // sq rows of this wave's chain lane group k
   double a_std = 0.0, a_m = 0.0, a_m2 = 0.0;
   const int NT = a.NT;
   const double dn = n;
   int64_t jg = jlo;
   if (jg < jhi) stage_load(jg);
   for (; jg < jhi; jg += 4) {
+    int nn = n;                                   // opaque per group: bounds recomputed, not hoisted
+    asm volatile("" : "+s"(nn));
 #ifndef HMC_MFMA_DEV_NOSTAGE                      // dev timing variant: matrix work on stale LDS
     __syncthreads();                              // the previous group's slices are read
-    stage_store();
+    stage_store(nn);
     __syncthreads();
     if (jg + 4 < jhi) stage_load(jg + 4);         // in flight under this group's matrix work
 #endif
     if (d < D) {
-      double ps1 = 0.0, ps2 = 0.0;
-      // the step bounds are recomputed per group from an opaque copy of n: hoisted out of the
-      // group loop, the 256 tile tests were live scalar masks (spilled)
-      int nn = n;
-      asm volatile("" : "+s"(nn));
-      // software-pipelined: the next tile's A slice and the next step's B slice are read one MFMA
-      // ahead (unconditionally up to the largest tile any n <= kMfmaMaxN runs at this step; the LDS
-      // carries slack past the last series for those reads)
-      double bn = ser[-c16];                      // B of step 0
+      int zo = (wv * 4 + k) * P + 16;             // (an opaque integer offset keeps sr an LDS pointer)
+      asm volatile("" : "+v"(zo));
+      const double* sr = lds + zo;
+      // Anchor steps b = 16 bi + 15 (anchors b - 15 .. b: step 0 starts at anchor 0).  Tile ti
+      // (T = 16 (ti - 1)) runs the steps whose anchors still meet a lag >= max(T, 0) below n:
+      // ti <= tl(bi) = v + 1 - bi, v = (n - 1) / 16, bi <= v.  Step-major: a step's tiles are
+      // independent accumulators back to back (a tile's own chain of dependent MFMAs ran 20-40 %
+      // slower).  Tile ti at step bi reads A slice q = bi + ti (rows 16 (q - 1) + 15 + t'): the
+      // slices q = 0 .. NTM are read once, up front, into registers; B of the next step is read a
+      // step ahead.  Reads past row n + 29 land in the next series or the LDS slack, feed no MFMA.
+      const int v = (nn - 1) >> 4;
+      double sl[NTM + 1];
+#pragma unroll
+      for (int q = 0; q <= NTM; ++q) sl[q] = sr[16 * (q - 1) + 15 + c16];
+      double bcur = sr[15 - c16];
       auto bstep = [&](auto bi_c) {
         constexpr int bi = decltype(bi_c)::value;
-        constexpr int TLS = (kMfmaMaxN + 14 - 16 * bi) / 16 + 1 < kMfmaNT - 1 ? (kMfmaMaxN + 14 - 16 * bi) / 16 + 1
-                                                                                 : kMfmaNT - 1;
-        if (16 * bi <= nn + 14) {
-          // last tile whose lags (>= T) still meet an anchor >= 16 bi - 15: 16 (ti - 1) <= n + 14 - 16 bi
-          const int tl = min(NT - 1, (nn + 14 - 16 * bi) / 16 + 1);
-          const double bv = bn;
-          if constexpr (bi + 1 < kMfmaNB) bn = ser[16 * (bi + 1) - c16];
-          double an = ser[16 * bi - 16 + c16];    // tile 0 (T = -16)
-          auto tile = [&](auto ti_c) {
-            constexpr int ti = decltype(ti_c)::value;
-            if constexpr (ti <= TLS) {
-              const double av = an;
-              if constexpr (ti + 1 <= TLS) an = ser[16 * bi + 16 * ti + c16];
-              if (ti <= tl) {
-                if constexpr (ti == 1 && bi < kMfmaRows) {   // T = 0: rows 16 bi + t' (moments, sq)
-                  const double a2 = av * av;
-                  ps1 += av;
-                  ps2 += a2;
-                  sqm[bi] += a2;
-                }
+        const int tl = min(NT - 1, v + 1 - bi);
+        const double bnx = bi + 1 < kNB ? sr[16 * (bi + 1) + 15 - c16] : 0.0;
+        auto tile = [&](auto ti_c) {
+          constexpr int ti = decltype(ti_c)::value;
+          if constexpr (bi + ti <= NTM) {
+            if (ti <= tl) {
 #ifdef HMC_MFMA_DEV_NOLDS                         // dev timing variant: no LDS operands
-                acc[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(dn, dn, acc[ti], 0, 0, 0);
+              acc[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(dn, dn, acc[ti], 0, 0, 0);
 #else
-                acc[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[ti], 0, 0, 0);
+              acc[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(sl[bi + ti], bcur, acc[ti], 0, 0, 0);
 #endif
-              }
             }
-          };
-          static_for<kMfmaNT>(tile);
-        }
+          }
+        };
+        static_for<NTM>(tile);
+        bcur = bnx;
       };
-      static_for<kMfmaNB>(bstep);
-      // split moments of chain k: reduce the 16 row phases (fixed xor order)
+      static_for<kNB>(bstep);
+      // split moments of chain k and the sq rows from the slices q = 0 .. kRows (rows
+      // 16 (q - 1) + 15 + t': every row once; row -1 and rows >= n are zeros or masked), the 16 row
+      // phases reduced in a fixed xor order
+      double ps1 = 0.0, ps2 = 0.0;
+      double sv[kRows + 1];
+#pragma unroll
+      for (int q = 0; q <= kRows; ++q) sv[q] = sqa[16 * q + c16];
+#pragma unroll
+      for (int q = 0; q <= kRows; ++q) {
+        const double y = 16 * (q - 1) + 15 + c16 < nn ? sl[q] : 0.0;
+        const double y2 = y * y;
+        ps1 += y;
+        ps2 += y2;
+        sqa[16 * q + c16] = sv[q] + y2;           // sq row 16 q + t' - 1
+      }
 #pragma unroll
       for (int m = 1; m < 16; m <<= 1) {
         ps1 += __shfl_xor(ps1, m, 64);
@@ -720,18 +744,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       }
     }
   }
-  // partial of this wave: tiles (entry t' * 16 + s), sq rows (summed over the 4 chain lanes), moments
+  // partial of this wave: tiles (entry t' * 16 + s), sq rows (summed over the 4 chain lanes; LDS
+  // entry i holds row i - 1), moments
   double* out = partial + ((int64_t)id * kMfmaDims + wv) * kMfmaPW;
 #pragma unroll
-  for (int t = 0; t < kMfmaNT; ++t)
+  for (int t = 0; t < NTM; ++t)
 #pragma unroll
     for (int q = 0; q < 4; ++q) out[t * 256 + q * 64 + lane] = acc[t][q];
+  {
+    const double* sw4 = sqb + wv * 4 * 256;
 #pragma unroll
-  for (int i = 0; i < kMfmaRows; ++i) {
-    double v = sqm[i];
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    if (lane < 16) out[kMfmaNT * 256 + 16 * i + lane] = v;
+    for (int i = 0; i < 4; ++i) {
+      const int row = 64 * i + lane;              // output row; LDS entry row + 1
+      double v = 0.0;
+      if (row < 255)
+        v = ((sw4[row + 1] + sw4[256 + row + 1]) + sw4[512 + row + 1]) + sw4[768 + row + 1];
+      out[kMfmaNT * 256 + row] = v;
+    }
   }
   a_std += __shfl_xor(a_std, 16, 64);
   a_std += __shfl_xor(a_std, 32, 64);
@@ -1110,7 +1139,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T <= 16 ? 3
 
 int64_t rows_chunks(int64_t rows) { return (rows + kRowChunk - 1) / kRowChunk; }
 
-// The matrix-core pass's geometry: ranges R (a multiple of 8) picked so that R x G workgroups (one
+// The matrix-core pass's geometry: ranges R (a multiple of 8) picked so that R x G workgroups (8 waves
 // per CU at a time) end in as full a last round as possible, at least 4 rounds.
 MfmaArgs mfma_args(const Src& s) {
   MfmaArgs a{};
@@ -1122,7 +1151,7 @@ MfmaArgs mfma_args(const Src& s) {
   a.G = (s.D + kMfmaDims - 1) / kMfmaDims;
   const int64_t m2 = n_series(s);
   const int64_t groups = (m2 + 3) / 4;
-  const int cus = device_cus();
+  const int cus = device_cus() * 2;              // workgroups resident at a time (2 waves per SIMD)
   int best = 8;
   double best_eff = -1.0;
   for (int x = 1; x <= 64; ++x) {
@@ -1147,8 +1176,10 @@ bool mfma_ok(const Src& s, int T) {
          n_series(s) >= 4;
 }
 
-// samples, x0, and slack for the pipelined reads past the last series (rows up to 16 + 285)
-size_t mfma_lds(const MfmaArgs& a) { return (size_t)(32 * a.P + 32 + 320) * sizeof(double); }
+// the samples, x0, the slack for the read-ahead past the last series, the sq rows
+size_t mfma_lds(const MfmaArgs& a) {
+  return (size_t)(kMfmaSer * a.P + kMfmaSer + kMfmaSlack + kMfmaSer * 256) * sizeof(double);
+}
 
 int64_t mfma_work(const MfmaArgs& a) {
   return (int64_t)a.R * a.G * kMfmaDims * kMfmaPW + (int64_t)a.s.D * kMfmaPW;
@@ -1158,7 +1189,9 @@ hipError_t launch_conv_mfma(const Src& s, int nlag, double* work, double* out, h
   const MfmaArgs a = mfma_args(s);
   double* partial = work;
   double* red = work + (int64_t)a.R * a.G * kMfmaDims * kMfmaPW;
-  k_conv_mfma<<<(unsigned)(a.R * a.G), 512, mfma_lds(a), st>>>(a, partial);
+  const unsigned grid = (unsigned)(a.R * a.G);
+  if (s.n <= 16 * 11) k_conv_mfma<12><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
+  else k_conv_mfma<14><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
   if (hipError_t e = hipGetLastError()) return e;
   const int64_t nr = (int64_t)s.D * kMfmaPW;
   k_mfma_ranges<<<(unsigned)((nr + 255) / 256), 256, 0, st>>>(a, partial, red);
