@@ -588,11 +588,13 @@ constexpr int kMfmaDims = 4;                     // waves (dimensions) per workg
 constexpr int kMfmaThreads = 64 * kMfmaDims;
 constexpr int kMfmaSer = 4 * kMfmaDims;          // series staged per chain group
 constexpr int kMfmaSlack = 320;                  // doubles past the last series (read-ahead)
+constexpr int kSqStride = 272;                   // sq rows per lane group (2176 B: bank-spread)
 constexpr int kMfmaPW = kMfmaNT * 256 + 256 + 4; // partial doubles per wave: tiles, sq rows, moments
 
 struct MfmaArgs {
   Src s;
-  int P;            // LDS doubles per series (rows -16 .. n + 29, stride = 16 mod 32)
+  int P;            // LDS doubles between dims' series (rows -16 .. n + 29; 8 mod 32)
+  int PK;           // between chains' (4 P + 16: 16 mod 32)
   int NT, NB;       // tiles and anchor steps used
   int G;            // dimension groups ceil(D / kMfmaDims)
   int R;            // split-chain ranges (a multiple of 8)
@@ -604,7 +606,8 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
                                                                                              double* partial) {
   // capacity of this instance: NTM tiles, NTM - 1 anchor steps, n <= 16 (NTM - 1)
   constexpr int kNB = NTM - 1, kRows = NTM - 1;
-  // LDS: [dims][4 chains][P] samples, x0[16], slack, sq rows [dims][4 chain lanes][256]
+  // LDS: [4 chains][dims] series of the group at k PK + w P (bank-spread for both the staging writes
+  // and the matrix waves' slice reads), x0[16], slack, sq rows [dims][4 chain lanes][272]
   extern __shared__ double lds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
@@ -614,16 +617,16 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
   const int local = id >> 3;
   const int r = (local / a.G) * 8 + (id & 7), g = local % a.G;
   const Src& s = a.s;
-  const int n = s.n, D = s.D, P = a.P;
-  const int SB = kMfmaSer * P;
+  const int n = s.n, D = s.D, P = a.P, PK = a.PK;
+  const int SB = 4 * PK;
   double* const x0l = lds + SB;
   double* const sqb = x0l + kMfmaSer + kMfmaSlack;
   const int64_t m2 = n_series(s);
   const int64_t jlo = (int64_t)r * a.per;
   const int64_t jhi = jlo + a.per < m2 ? jlo + a.per : m2;
-  for (int i = tid; i < SB + kMfmaSer + kMfmaSlack + kMfmaSer * 256; i += kMfmaThreads) lds[i] = 0.0;
-  // staging role: thread = (dim sw, chain sk of the group, row phase rho); rows rho + 16 i
-  const int sw = tid % kMfmaDims, sk = (tid / kMfmaDims) & 3, rho = tid / (4 * kMfmaDims);
+  for (int i = tid; i < SB + kMfmaSer + kMfmaSlack + kMfmaSer * kSqStride; i += kMfmaThreads) lds[i] = 0.0;
+  // staging role: wave = chain sk of the group, lane = (dim sw, row phase rho); rows rho + 16 i
+  const int sk = wv, sw = lane & 3, rho = lane >> 2;
   const int sd = g * kMfmaDims + sw;
   double xs[kRows];
   double x0s = 0.0;
@@ -648,13 +651,13 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
     }
   };
   auto stage_store = [&](int nn) {
-    double* dst = lds + (sw * 4 + sk) * P + 16;
+    double* dst = lds + sk * PK + sw * P + 16;
 #pragma unroll
     for (int i = 0; i < kRows; ++i) {
       const int row = rho + 16 * i;
       if (row < nn) dst[row] = sok ? xs[i] - x0s : 0.0;   // rows >= n stay zero
     }
-    if (rho == 0) x0l[sw * 4 + sk] = sok ? x0s : 0.0;
+    if (rho == 0) x0l[sk * 4 + sw] = sok ? x0s : 0.0;
   };
   // matrix role: wave wv = dimension d; lane = (chain k = lane >> 4, t' or s = lane & 15)
   const int d = g * kMfmaDims + wv;
@@ -664,7 +667,7 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
   v4d acc[NTM];
 #pragma unroll
   for (int t = 0; t < NTM; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
-  double* const sqa = sqb + (wv * 4 + k) * 256;   // sq rows of this wave's chain lane group k
+  double* const sqa = sqb + (wv * 4 + k) * kSqStride;   // sq rows of this wave's chain lane group k
   double a_std = 0.0, a_m = 0.0, a_m2 = 0.0;
   const int NT = a.NT;
   const double dn = n;
@@ -680,7 +683,7 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
     if (jg + 4 < jhi) stage_load(jg + 4);         // in flight under this group's matrix work
 #endif
     if (d < D) {
-      int zo = (wv * 4 + k) * P + 16;             // (an opaque integer offset keeps sr an LDS pointer)
+      int zo = k * PK + wv * P + 16;              // (an opaque integer offset keeps sr an LDS pointer)
       asm volatile("" : "+v"(zo));
       const double* sr = lds + zo;
       // Anchor steps b = 16 bi + 15 (anchors b - 15 .. b: step 0 starts at anchor 0).  Tile ti
@@ -738,7 +741,7 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
       if (jg + k < jhi) {
         const double mm2 = ps2 - ps1 * ps1 / dn;
         a_std += sqrt(mm2 > 0.0 ? mm2 / (dn - 1.0) : 0.0);
-        const double e = (x0l[wv * 4 + k] - Sd) + ps1 / dn;
+        const double e = (x0l[k * 4 + wv] - Sd) + ps1 / dn;
         a_m += e;
         a_m2 = __builtin_fma(e, e, a_m2);
       }
@@ -752,13 +755,13 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
 #pragma unroll
     for (int q = 0; q < 4; ++q) out[t * 256 + q * 64 + lane] = acc[t][q];
   {
-    const double* sw4 = sqb + wv * 4 * 256;
+    const double* sw4 = sqb + wv * 4 * kSqStride;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = 64 * i + lane;              // output row; LDS entry row + 1
       double v = 0.0;
       if (row < 255)
-        v = ((sw4[row + 1] + sw4[256 + row + 1]) + sw4[512 + row + 1]) + sw4[768 + row + 1];
+        v = ((sw4[row + 1] + sw4[kSqStride + row + 1]) + sw4[2 * kSqStride + row + 1]) + sw4[3 * kSqStride + row + 1];
       out[kMfmaNT * 256 + row] = v;
     }
   }
@@ -1145,7 +1148,8 @@ MfmaArgs mfma_args(const Src& s) {
   MfmaArgs a{};
   a.s = s;
   const int n = s.n;
-  a.P = 32 * ((n + 46 - 16 + 31) / 32) + 16;
+  a.P = 32 * ((n + 46 - 8 + 31) / 32) + 8;
+  a.PK = 4 * a.P + 16;
   a.NT = (n - 1) / 16 + 2;
   a.NB = (n + 14) / 16 + 1;
   a.G = (s.D + kMfmaDims - 1) / kMfmaDims;
@@ -1178,7 +1182,7 @@ bool mfma_ok(const Src& s, int T) {
 
 // the samples, x0, the slack for the read-ahead past the last series, the sq rows
 size_t mfma_lds(const MfmaArgs& a) {
-  return (size_t)(kMfmaSer * a.P + kMfmaSer + kMfmaSlack + kMfmaSer * 256) * sizeof(double);
+  return (size_t)(4 * a.PK + kMfmaSer + kMfmaSlack + kMfmaSer * kSqStride) * sizeof(double);
 }
 
 int64_t mfma_work(const MfmaArgs& a) {
