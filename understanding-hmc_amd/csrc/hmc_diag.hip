@@ -630,34 +630,32 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
   const int sd = g * kMfmaDims + sw;
   double xs[kRows];
   double x0s = 0.0;
-  bool sok = false;
   // buffer loads based at the group's first split chain (uniform): one 32-bit lane offset (host-
-  // checked below kLagOOB; lanes past the range or the dims read zeros), rows clamped to n - 1 and
-  // recomputed per group (hoisted, 13 row addresses stayed live through the matrix loop)
+  // checked below kLagOOB) plus 16 i rows (in the vector offset: the range check covers it); the
+  // buffer ends with the view's last sample, so lanes past the range or the dims (offset kLagOOB)
+  // and rows past the last chain's end read zeros (y = 0 - 0)
   const int rowb = (int)(s.sample_stride * 8);
+  const double* const vend = split_ptr(s, m2 - 1, n - 1) + D;
   auto stage_load = [&](int64_t jg) {
     const int64_t j = jg + sk;
-    sok = sd < D && j < jhi;
     const double* b = uni(split_ptr(s, jg, 0));
-    const int lo = sok ? (int)((split_ptr(s, j, 0) - b) + sd) * 8 : kLagOOB + 64;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(b), 0, kLagOOB, 0x00020000);
-    int ro = rho;
-    asm volatile("" : "+v"(ro));
-    x0s = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lo, 0, 0));
+    const int64_t span = (vend - b) * 8;
+    const int nrec = span < kLagOOB ? (int)span : kLagOOB;
+    const int lo = (sd < D && j < jhi) ? (int)((split_ptr(s, j, 0) - b) + sd) * 8 + rho * rowb : kLagOOB + 64;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(b), 0, nrec, 0x00020000);
+    x0s = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lo - rho * rowb, 0, 0));
 #pragma unroll
-    for (int i = 0; i < kRows; ++i) {
-      const int row = min(ro + 16 * i, n - 1);
-      xs[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lo + row * rowb, 0, 0));
-    }
+    for (int i = 0; i < kRows; ++i)
+      xs[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lo + 16 * i * rowb, 0, 0));
   };
   auto stage_store = [&](int nn) {
-    double* dst = lds + sk * PK + sw * P + 16;
+    double* dst = lds + sk * PK + sw * P + 16 + rho;
 #pragma unroll
     for (int i = 0; i < kRows; ++i) {
-      const int row = rho + 16 * i;
-      if (row < nn) dst[row] = sok ? xs[i] - x0s : 0.0;   // rows >= n stay zero
+      if (16 * i + 15 < nn) dst[16 * i] = xs[i] - x0s;                    // whole 16-row phase
+      else if (16 * i < nn && rho + 16 * i < nn) dst[16 * i] = xs[i] - x0s;   // rows >= n stay zero
     }
-    if (rho == 0) x0l[sk * 4 + sw] = sok ? x0s : 0.0;
+    if (rho == 0) x0l[sk * 4 + sw] = x0s;
   };
   // matrix role: wave wv = dimension d; lane = (chain k = lane >> 4, t' or s = lane & 15)
   const int d = g * kMfmaDims + wv;
@@ -671,6 +669,7 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
   double a_std = 0.0, a_m = 0.0, a_m2 = 0.0;
   const int NT = a.NT;
   const double dn = n;
+  const double rn = 1.0 / dn, rn1 = 1.0 / (dn - 1.0);
   int64_t jg = jlo;
   if (jg < jhi) stage_load(jg);
   for (; jg < jhi; jg += 4) {
@@ -725,13 +724,15 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
       double sv[kRows + 1];
 #pragma unroll
       for (int q = 0; q <= kRows; ++q) sv[q] = sqa[16 * q + c16];
+      const int qn = nn >> 4;                     // slices past q = n / 16 hold rows >= n only
 #pragma unroll
       for (int q = 0; q <= kRows; ++q) {
-        const double y = 16 * (q - 1) + 15 + c16 < nn ? sl[q] : 0.0;
-        const double y2 = y * y;
-        ps1 += y;
-        ps2 += y2;
-        sqa[16 * q + c16] = sv[q] + y2;           // sq row 16 q + t' - 1
+        if (q <= qn) {                            // (rows n .. n + 29 of slice qn are LDS zeros)
+          const double y = sl[q];
+          ps1 += y;
+          ps2 = __builtin_fma(y, y, ps2);
+          sqa[16 * q + c16] = __builtin_fma(y, y, sv[q]);   // sq row 16 q + t' - 1
+        }
       }
 #pragma unroll
       for (int m = 1; m < 16; m <<= 1) {
@@ -739,9 +740,9 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
         ps2 += __shfl_xor(ps2, m, 64);
       }
       if (jg + k < jhi) {
-        const double mm2 = ps2 - ps1 * ps1 / dn;
-        a_std += sqrt(mm2 > 0.0 ? mm2 / (dn - 1.0) : 0.0);
-        const double e = (x0l[k * 4 + wv] - Sd) + ps1 / dn;
+        const double mm2 = ps2 - ps1 * (ps1 * rn);
+        a_std += sqrt(mm2 > 0.0 ? mm2 * rn1 : 0.0);
+        const double e = (x0l[k * 4 + wv] - Sd) + ps1 * rn;
         a_m += e;
         a_m2 = __builtin_fma(e, e, a_m2);
       }
@@ -1175,9 +1176,11 @@ MfmaArgs mfma_args(const Src& s) {
   return a;
 }
 
+// (the staging's 32-bit lane offsets: four split chains = two chains' rows from a group's first)
 bool mfma_ok(const Src& s, int T) {
+  const int64_t span = (2 * s.chain_stride + 2 * (int64_t)s.n * s.sample_stride + s.D) * 8;
   return s.halves == 2 && s.wrap == 0 && s.n >= kMfmaMinN && s.n <= kMfmaMaxN && T >= s.n - 2 &&
-         n_series(s) >= 4;
+         n_series(s) >= 4 && s.chain_stride >= (int64_t)s.n * s.sample_stride && span < kLagOOB;
 }
 
 // the samples, x0, the slack for the read-ahead past the last series, the sq rows
