@@ -111,7 +111,8 @@ def test_convergence_stats_long_lags_vs_oracle(thin, wu):
     (utils.py:77-179 restated)."""
     from hmc_amd import diagnostics as G
     rs = np.random.RandomState(3)
-    N, L, D, rho = 20, 601, 12, np.linspace(0.3, 0.997, 12)
+    # split halves of n = 300 (thin 1) and 299 (thin 3): past the complete pass (n - 1 <= 256)
+    N, L, D, rho = 20, 601 if thin == 1 else 1801, 12, np.linspace(0.3, 0.997, 12)
     x = np.empty((N, L, D))
     x[:, 0] = rs.standard_normal((N, D)) + 3.0
     for t in range(1, L):
