@@ -41,7 +41,11 @@ def _half_expected(x, tmax):
                                            (3, 200, 70, 240, 239),   # wraps after one sample
                                            (40, 17, 1000, 30, 0),    # no wrap, D = 1000
                                            (5, 57, 33, 57, 20),      # the half fills the window
-                                           (9, 4, 64, 8, 6)])        # tiny half
+                                           (9, 4, 64, 8, 6),         # tiny half
+                                           # halves of 128 .. 208 that do not wrap: the matrix cores
+                                           (6, 199, 100, 420, 201),  # c4 at 400 samples: the second half
+                                           (3, 130, 13, 131, 0),     # D = 13, three series (< one group)
+                                           (9, 208, 40, 208, 0)])    # the largest, the window exactly
 def test_half_sums_circular_window_vs_numpy(N, n, D, W, slot0):
     from hmc_amd import _lib as H
     rng = np.random.default_rng(N + n + D + W)

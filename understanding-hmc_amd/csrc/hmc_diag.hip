@@ -1176,11 +1176,14 @@ MfmaArgs mfma_args(const Src& s) {
   return a;
 }
 
-// (the staging's 32-bit lane offsets: four split chains = two chains' rows from a group's first)
+// Stored split chains (halves 2) or completed halves of a streaming window that do not wrap
+// (halves 1, wrap 0).  The staging's 32-bit lane offsets span a group's four series: two chains'
+// rows (split chains) or four chains' (halves).
 bool mfma_ok(const Src& s, int T) {
-  const int64_t span = (2 * s.chain_stride + 2 * (int64_t)s.n * s.sample_stride + s.D) * 8;
-  return s.halves == 2 && s.wrap == 0 && s.n >= kMfmaMinN && s.n <= kMfmaMaxN && T >= s.n - 2 &&
-         n_series(s) >= 4 && s.chain_stride >= (int64_t)s.n * s.sample_stride && span < kLagOOB;
+  const int64_t rows = (int64_t)s.n * s.sample_stride;
+  const int64_t span = (s.halves == 2 ? 2 * s.chain_stride + 2 * rows : 3 * s.chain_stride + rows) + s.D;
+  return (s.halves == 2 || s.halves == 1) && s.wrap == 0 && s.n >= kMfmaMinN && s.n <= kMfmaMaxN &&
+         T >= s.n - 2 && n_series(s) >= 4 && s.chain_stride >= rows && span * 8 < kLagOOB;
 }
 
 // the samples, x0, the slack for the read-ahead past the last series, the sq rows
@@ -1338,8 +1341,10 @@ int64_t diag_conv_work(int64_t n_chains, int D, int T) {
   // a complete pass of split chains of kMfmaMinN .. T + 2 samples may take the matrix cores (their
   // geometry depends on the chains and dims only)
   if (T + 2 >= kMfmaMinN) {
-    Src s{nullptr, 0, 0, 0, n_chains, kMfmaMinN, D};
-    w = std::max(w, mfma_work(mfma_args(s)));
+    for (int halves = 1; halves <= 2; ++halves) {   // stored split chains, or streaming halves
+      Src s{nullptr, 0, 0, 0, n_chains, kMfmaMinN, D, halves};
+      w = std::max(w, mfma_work(mfma_args(s)));
+    }
   }
   return w;
 }
@@ -1359,6 +1364,9 @@ hipError_t launch_half_sums(const double* x, int64_t n_chains, int64_t cs, int64
   if (wrap > 0 && slot0 + n <= wrap) wrap = 0;
   Src s{x, cs, ss, 0, n_chains, n, D, 1, wrap, slot0};
   if (wrap <= 0) s.base = (int64_t)slot0 * ss;   // no wrap: sample s in row slot0 + s
+#ifndef HMC_LAG_NO_MFMA
+  if (mfma_ok(s, T)) return launch_conv_mfma(s, T, work, out, st);
+#endif
   return launch_lags(s, 0, T, 1, 1, 0, T, work, out, st);
 }
 
