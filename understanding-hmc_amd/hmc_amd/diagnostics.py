@@ -477,7 +477,9 @@ class StreamingDiagnostics:
         assert self.n <= window.shape[1], "the window must hold a whole half"
         T = self.exact_lags()
         L = H.lib()
-        work = self._z(max(1, L.hmc_convergence_work_size(self.N, self.D, T)))
+        # (the kernels write every work entry they read: no zero fill)
+        work = torch.empty(max(1, L.hmc_convergence_work_size(self.N, self.D, T)), dtype=torch.float64,
+                           device=self.device)
         out = self._z(4 + T, self.D)
         Wr = window.shape[1]
         H.check(L.hmc_half_sums(window.data_ptr(), self.N, window.stride(0), window.stride(1), self.D, Wr,
