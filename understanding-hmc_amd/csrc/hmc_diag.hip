@@ -564,7 +564,7 @@ __global__ __launch_bounds__(256) void k_lag_dims(LagArgs a, const double* __res
   out[i] = acc;
 }
 
-// ---- The same one-read sums on the matrix cores (stored complete passes, 128 <= n <= 208: c3's
+// ---- The same one-read sums on the matrix cores (complete passes, 96 <= n <= 208: c3's
 // n = 200).  The lag products are GEMM-shaped once the series is laid out as Hankel slices:
 // v_mfma_f64_16x16x4_f64 with A[t'][k] = y_k[b + T + t'] and B[k][s] = y_k[b - s] (k = four split
 // chains of ONE dimension, the contraction index) adds y_k[i] y_k[i + L] to entry (t', s) of tile T,
@@ -583,7 +583,10 @@ __global__ __launch_bounds__(256) void k_lag_dims(LagArgs a, const double* __res
 // within a few ulps of np.mean's sequential sum).
 constexpr int kMfmaNT = 16;                      // tiles T = -16 .. 16 (kMfmaNT - 2)
 constexpr int kMfmaMaxN = 16 * (kMfmaNT - 3);    // 208 samples per split chain (NTM = 14)
-constexpr int kMfmaMinN = 128;
+#ifndef HMC_MFMA_MIN_N
+#define HMC_MFMA_MIN_N 96
+#endif
+constexpr int kMfmaMinN = HMC_MFMA_MIN_N;
 constexpr int kMfmaDims = 4;                     // waves (dimensions) per workgroup
 constexpr int kMfmaThreads = 64 * kMfmaDims;
 constexpr int kMfmaSer = 4 * kMfmaDims;          // series staged per chain group
@@ -1200,7 +1203,10 @@ hipError_t launch_conv_mfma(const Src& s, int nlag, double* work, double* out, h
   double* partial = work;
   double* red = work + (int64_t)a.R * a.G * kMfmaDims * kMfmaPW;
   const unsigned grid = (unsigned)(a.R * a.G);
-  if (s.n <= 16 * 11) k_conv_mfma<12><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
+  if (s.n <= 16 * 5) k_conv_mfma<6><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
+  else if (s.n <= 16 * 7) k_conv_mfma<8><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
+  else if (s.n <= 16 * 9) k_conv_mfma<10><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
+  else if (s.n <= 16 * 11) k_conv_mfma<12><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
   else k_conv_mfma<14><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
   if (hipError_t e = hipGetLastError()) return e;
   const int64_t nr = (int64_t)s.D * kMfmaPW;
