@@ -279,7 +279,9 @@ hmc_status hmc_variogram(const double* x, int64_t n_chains, int64_t chain_stride
  * (the view's first sample: a common shift so that B needs no second pass).  1 <= tmax <= 2^20:
  * the window is read once whatever tmax (ramp-skipping lag kernel); tmax >= n - 2 gives every lag
  * the ESS loop can read (the last few in difference form); more lags later for a subset of dims:
- * hmc_variogram.  Deterministic (fixed-order two-stage sums). */
+ * hmc_variogram.  Complete passes (tmax >= n - 2) of 96 <= n <= 208 run on the f64 matrix cores
+ * (lag products as Hankel-tile MFMAs; split means from partial sums in a fixed order, within a few
+ * ulps of np.mean's sequential sum).  Deterministic (fixed-order two-stage sums). */
 int64_t hmc_convergence_work_size(int64_t n_chains, int32_t D, int32_t tmax);
 hmc_status hmc_convergence_sums(const double* x, int64_t n_chains, int64_t chain_stride, int64_t sample_stride,
                                 int64_t base, int32_t n, int32_t D, int32_t tmax, double* work, double* out,
