@@ -669,6 +669,12 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
 #pragma unroll
   for (int t = 0; t < NTM; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
   double* const sqa = sqb + (wv * 4 + k) * kSqStride;   // sq rows of this wave's chain lane group k
+  // the small instances keep the sq rows in registers instead (they have the room: no LDS
+  // read-modify-write per group)
+  constexpr bool SQR = NTM <= 10;
+  double sqr[SQR ? NTM : 1];
+#pragma unroll
+  for (int q = 0; q < (SQR ? NTM : 1); ++q) sqr[q] = 0.0;
   double a_std = 0.0, a_m = 0.0, a_m2 = 0.0;
   const int NT = a.NT;
   const double dn = n;
@@ -726,7 +732,7 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
       double ps1 = 0.0, ps2 = 0.0;
       double sv[kRows + 1];
 #pragma unroll
-      for (int q = 0; q <= kRows; ++q) sv[q] = sqa[16 * q + c16];
+      for (int q = 0; q <= kRows; ++q) sv[q] = SQR ? 0.0 : sqa[16 * q + c16];
       const int qn = nn >> 4;                     // slices past q = n / 16 hold rows >= n only
 #pragma unroll
       for (int q = 0; q <= kRows; ++q) {
@@ -734,7 +740,8 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
           const double y = sl[q];
           ps1 += y;
           ps2 = __builtin_fma(y, y, ps2);
-          sqa[16 * q + c16] = __builtin_fma(y, y, sv[q]);   // sq row 16 q + t' - 1
+          if constexpr (SQR) sqr[q] = __builtin_fma(y, y, sqr[q]);
+          else sqa[16 * q + c16] = __builtin_fma(y, y, sv[q]);   // sq row 16 q + t' - 1
         }
       }
 #pragma unroll
@@ -758,7 +765,16 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
   for (int t = 0; t < NTM; ++t)
 #pragma unroll
     for (int q = 0; q < 4; ++q) out[t * 256 + q * 64 + lane] = acc[t][q];
-  {
+  if constexpr (SQR) {                            // rows 16 q + t' - 1, summed over the 4 lane groups
+#pragma unroll
+    for (int q = 0; q <= kRows; ++q) {
+      double v = sqr[q];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const int row = 16 * q + c16 - 1;
+      if (lane < 16 && row >= 0) out[kMfmaNT * 256 + row] = v;
+    }
+  } else {
     const double* sw4 = sqb + wv * 4 * kSqStride;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
