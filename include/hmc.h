@@ -169,6 +169,21 @@ hmc_status hmc_chain_init(const hmc_target* t, const hmc_kinetic* k, const hmc_s
 hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s,
                             const hmc_replay* r /* NULL for Philox */, hmc_state* st, void* stream);
 
+/* The same two calls with the size of hmc_state.order (bytes) passed alongside: HMC_EINVAL when
+ * it is smaller than this call reads or writes (hmc_random_workspace_size_ex), before any kernel
+ * runs.  The size is also recorded for the buffer, so that the unsized forms above refuse it later
+ * if a call needs more (as they refuse any buffer recorded by hmc_workspace_register). */
+hmc_status hmc_chain_init_ws(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s,
+                             const hmc_replay* r, const double* q_start, hmc_state* st,
+                             int64_t order_bytes, void* stream);
+hmc_status hmc_random_iters_ws(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s,
+                               const hmc_replay* r, hmc_state* st, int64_t order_bytes, void* stream);
+
+/* Record the size of a scratch buffer (hmc_state.order or a NUTS workspace) for the unsized entry
+ * points: a later call that would need more than `bytes` returns HMC_EINVAL instead of writing past
+ * the end.  bytes = 0 forgets the buffer.  Host-side bookkeeping only (no device access). */
+hmc_status hmc_workspace_register(const void* workspace, int64_t bytes);
+
 /* Bytes of the optional hmc_state.order scratch for hmc_random_iters on this target
  * (0 for diagonal targets, which need none): the tile order plus the gradient cache.  Large-D
  * targets (dense D > 128, diagonal D > 2048) keep their chain state there and need it, also for
@@ -212,6 +227,8 @@ int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max);
 hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s,
                           const hmc_replay* r /* NULL for Philox */, hmc_state* st, void* workspace,
                           void* stream);
+/* hmc_nuts_iters_ws: the sized form (records workspace_bytes for the buffer; the unsized form then
+ * refuses it for any call that needs more, as for hmc_workspace_register). */
 hmc_status hmc_nuts_iters_ws(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s,
                              const hmc_replay* r /* NULL for Philox */, hmc_state* st, void* workspace,
                              int64_t workspace_bytes, void* stream);

@@ -153,3 +153,52 @@ def test_nuts_sized_entry_refuses_small_workspace(monkeypatch):
     none = L.hmc_nuts_workspace_size_ex(D, n, d_max, 32, 0)        # sized without Philox momenta
     with pytest.raises(AssertionError, match="needs"):
         H.check(L.hmc_nuts_iters_ws(T, K, S, None, st, 1, none, None), "x")
+
+
+def test_every_scratch_entry_refuses_undersized_workspace(monkeypatch):
+    """Every entry that takes device scratch refuses an undersized buffer on the host (HMC_EINVAL ->
+    AssertionError) before a kernel could write past its end (verdict r05 item 4): the sized forms
+    check the size they are given; the unsized forms check the size recorded for the buffer by a
+    sized call or hmc_workspace_register.  Fake device pointers: nothing reaches the GPU."""
+    from hmc_amd import _lib as H
+    monkeypatch.setattr(H, "_lib", None)
+    L = H.lib()
+    K = H.Kinetic(None, None, None, 0.1, None, None, None)
+    n = 1000
+    S = H.Schedule(n, 0, 100, 0, 1, 101, 5, 20, 1, 11, H.HMC_RNG_PHILOX, H.HMC_MODE_FAST, 10, 1, 0)
+    ORDER = 0x7000_0000                         # fake device pointers (never dereferenced here)
+    for D, kind in ((100, H.HMC_TARGET_DENSE), (200, H.HMC_TARGET_DENSE), (3000, H.HMC_TARGET_DIAG)):
+        T = H.Target(D, kind, None, 1 if kind == H.HMC_TARGET_DENSE else None, 0.0)
+        need = L.hmc_random_workspace_size_ex(ctypes.byref(T), ctypes.byref(K), n)
+        assert need > 0
+        st = H.State(1, 1)
+        st.order = ORDER
+        with pytest.raises(AssertionError, match="needs"):
+            H.check(L.hmc_random_iters_ws(T, K, S, None, st, need - 8, None), "x")
+        with pytest.raises(AssertionError, match="needs"):
+            H.check(L.hmc_chain_init_ws(T, K, S, None, 1, st, need - 8, None), "x")
+        # unsized forms: a buffer recorded as too small is refused the same way
+        assert L.hmc_workspace_register(ORDER, need - 8) == H.HMC_OK
+        with pytest.raises(AssertionError, match="needs"):
+            H.check(L.hmc_random_iters(T, K, S, None, st, None), "x")
+        with pytest.raises(AssertionError, match="needs"):
+            H.check(L.hmc_chain_init(T, K, S, None, 1, st, None), "x")
+        assert L.hmc_workspace_register(ORDER, 0) == H.HMC_OK    # forget it
+    # NUTS: the unsized entry refuses a workspace a sized call (or the caller) recorded as smaller
+    D, d_max = 100, 10
+    T = H.Target(D, H.HMC_TARGET_DENSE, None, 1, 0.0)
+    st = H.State(1, 1)
+    S32 = H.Schedule(n, 0, 100, 0, 1, 101, 5, 20, 1, 33, H.HMC_RNG_PHILOX, H.HMC_MODE_FAST, d_max, 1, 0)
+    WS = 0x7100_0000
+    small = L.hmc_nuts_workspace_size_ex(D, n, d_max, 8, 1)
+    assert L.hmc_workspace_register(WS, small) == H.HMC_OK
+    with pytest.raises(AssertionError, match="needs"):
+        H.check(L.hmc_nuts_iters(T, K, S32, None, st, WS, None), "x")
+    with pytest.raises(AssertionError, match="needs"):
+        H.check(L.hmc_nuts_iters_ws(T, K, S32, None, st, WS, small, None), "x")
+    assert L.hmc_workspace_register(WS, 0) == H.HMC_OK
+    # a NULL kinetic block is refused, not dereferenced
+    with pytest.raises(AssertionError):
+        H.check(L.hmc_nuts_iters_ws(T, None, S32, None, st, WS, small, None), "x")
+    with pytest.raises(AssertionError):
+        H.check(L.hmc_workspace_register(None, 8), "x")

@@ -53,10 +53,13 @@ CASES = [
     (5, 115, 70, 0, 1, 1, 55),         # n = 57: one group + the longest tail, 8
     (5, 117, 70, 0, 1, 1, 56),         # n = 58: two groups (a tail of 9 would exceed 8)
     (4, 240, 100, 0, 1, 1, 150),       # tmax beyond n - 1 = 119: the lags past it are 0
-    # complete passes of 128 <= n <= 240 take the matrix cores (k_conv_mfma, Hankel tiles)
-    (3, 257, 13, 0, 1, 1, 126),        # n = 128 (the smallest), D = 13: a partial dim group; 6 split
+    # complete passes of 96 <= n <= 208 take the matrix cores (k_conv_mfma, Hankel tiles;
+    # hmc_diag.hip kMfmaMinN / kMfmaMaxN)
+    (3, 193, 13, 0, 1, 1, 94),         # n = 96 (the smallest), D = 13: a partial dim group; 6 split
                                        # chains: one full chain group of 4 and a ragged one
-    (2, 481, 100, 0, 1, 1, 238),       # n = 240 (the largest): every tile and anchor step
+    (3, 257, 13, 0, 1, 1, 126),        # n = 128, the same groups
+    (2, 417, 100, 0, 1, 1, 206),       # n = 208 (the largest): every tile and anchor step
+    (2, 481, 100, 0, 1, 1, 238),       # n = 240: past the matrix-core range (VALU lag kernel)
     (5, 300, 101, 1, 1, 1, 200),       # n = 149, a D = 100 view with odd row stride; tmax beyond n - 1
     (4, 452, 9, -1, 1, 0, 224),        # storage at an 8-B offset, n = 226, odd D
     (7, 301, 64, 0, 1, 1, 148),        # n = 150, D = 64: full dim groups

@@ -153,6 +153,44 @@ def test_streaming_exact_checkpoint_resume(tmp_path):
     np.testing.assert_array_equal(neff, neff_ref)
 
 
+def test_streaming_checkpoint_inside_first_half(tmp_path):
+    """Checkpoint INSIDE split half 0 (exact mode chosen, nothing fed yet: diag.pos = 0, the open
+    half only in the window).  The checkpoint carries the mode and the window size (advisor r05): a
+    resume with another feed keeps exact mode and, when the window size is unchanged, matches the
+    uninterrupted run bit for bit; one whose feed asks for another window size is refused instead of
+    summing half 0 from a zeroed window."""
+    from hmc_amd.diagnostics import StreamingDiagnostics
+    make = _engine_pair(100, 128, 160, 20, 1, seed=5)
+
+    def diag(e):
+        return StreamingDiagnostics(e.N, e.D, e.L_chain - 1, tmax=16)
+    ref = make(False)
+    sref = diag(ref)
+    ref.run_streaming(sref, 1, 161, 10, feed=80)
+    R_ref, neff_ref = sref.finish()
+    a = make(False)
+    sa = diag(a)
+    a.run_streaming(sa, 1, 41, 10, feed=80)                   # rows 1..20 of half 0 (70 rows)
+    assert sa.pos == 0 and sa.halves == [] and sa.mode == "exact"
+    path = str(tmp_path / "c.npz")
+    a.save(path, 41, diag=sa)
+    # feed 20 alone would choose segment mode (n = 70 > tmax + 20); the recorded mode wins, and the
+    # window is the same 82 rows (one half + a launch of 10 rows + 2)
+    b = make(False)
+    sb = diag(b)
+    assert b.restore(path, diag=sb) == 41 and sb.mode == "exact" and sb.window_rows == 82
+    b.run_streaming(sb, 41, 161, 10, feed=20)
+    R, neff = sb.finish()
+    np.testing.assert_array_equal(R, R_ref)
+    np.testing.assert_array_equal(neff, neff_ref)
+    # feed 160 would hold both halves (152 rows): refused, the open half is not dropped
+    c = make(False)
+    sc = diag(c)
+    assert c.restore(path, diag=sc) == 41
+    with pytest.raises(AssertionError, match="window"):
+        c.run_streaming(sc, 41, 161, 10, feed=160)
+
+
 def test_convergence_stats_n200_one_pass():
     """c3's window shape (n = 200, slow mixing in every dim): one complete pass, no fallback."""
     from hmc_amd import diagnostics as G

@@ -7,7 +7,9 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 
 #include "hmc.h"
 #include "hmc_internal.hpp"
@@ -157,6 +159,38 @@ bool general_diag(const hmc_target* t, const hmc_kinetic* k) {
 
 constexpr int32_t kMaxLags = 1 << 20;   // lag passes of the diagnostics (any n the samples allow)
 
+// Host-side record of the scratch buffers' sizes (device pointer -> bytes): the sized entries
+// (*_ws) record what they were given, hmc_workspace_register records a caller's buffer, and every
+// entry that takes scratch refuses (HMC_EINVAL) a buffer recorded as smaller than the call needs,
+// before any kernel could write past its end.  No device access: the check stays graph-capturable.
+std::mutex g_ws_mu;
+std::unordered_map<const void*, int64_t> g_ws_bytes;
+
+void ws_record(const void* p, int64_t bytes) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  if (bytes > 0) g_ws_bytes[p] = bytes;
+  else g_ws_bytes.erase(p);
+}
+
+hmc_status ws_check(const void* p, int64_t need, const char* what) {
+  if (!p || need <= 0) return HMC_OK;
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  const auto it = g_ws_bytes.find(p);
+  if (it != g_ws_bytes.end() && it->second < need)
+    return fail(HMC_EINVAL, "%s: scratch buffer of %lld bytes, this call needs %lld", what, (long long)it->second,
+                (long long)need);
+  return HMC_OK;
+}
+
+// Bytes of hmc_state.order this Random-sampler call reads or writes (0: none).
+int64_t order_need(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, const hmc_state* st) {
+  if (!st->order || s->n_chains == 0) return 0;
+  const bool dense = t->kind == HMC_TARGET_DENSE;
+  if (hmc::big_path(dense, t->D)) return hmc::big_workspace_bytes(s->n_chains, t->D, dense, k->minv_full != nullptr);
+  return dense ? hmc::dense_workspace_bytes(s->n_chains, t->D) : 0;
+}
+
 hmc_status view_too_large(const char* what) {
   return fail(HMC_ENOTSUP,
               "%s: one chain's samples span more than the lag kernel's 1 GiB buffer offsets; pass fewer "
@@ -191,7 +225,7 @@ hmc_status hmc_chain_init(const hmc_target* t, const hmc_kinetic* k, const hmc_s
   if (!st->q || !st->E_prev || !q_start) return fail(HMC_EINVAL, "null state/q_start");
   const bool replay = s->rng_mode == HMC_RNG_REPLAY;
   if (replay && (!r || !r->p0)) return fail(HMC_EINVAL, "replay mode needs p0");
-  if (s->n_chains == 0) return HMC_OK;
+  if (hmc_status e = ws_check(st->order, order_need(t, k, s, st), "hmc_chain_init: state.order")) return e;
   const bool dense = t->kind == HMC_TARGET_DENSE;
   if (hmc::big_path(dense, t->D)) {   // large D: chain state in the workspace (hmc_big.hip)
     if (!st->order) return fail(HMC_EINVAL, "D=%d needs hmc_random_workspace_size() bytes in state.order", t->D);
@@ -237,6 +271,7 @@ hmc_status hmc_random_iters(const hmc_target* t, const hmc_kinetic* k, const hmc
   if (s->n_chains == 0 || s->iter_end == s->iter_begin) return HMC_OK;
   if (st->n_save > 0 && st->traj_q && st->traj_stride < s->L_high)
     return fail(HMC_EINVAL, "traj_stride must be >= L_high");
+  if (hmc_status e = ws_check(st->order, order_need(t, k, s, st), "hmc_random_iters: state.order")) return e;
   const bool dense = t->kind == HMC_TARGET_DENSE;
   if (hmc::big_path(dense, t->D)) {   // large D (hmc_big.hip)
     if (!st->order) return fail(HMC_EINVAL, "D=%d needs hmc_random_workspace_size() bytes in state.order", t->D);
@@ -331,22 +366,60 @@ int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max) {
                   hmc_nuts_workspace_size_ex(D, n_chains, d_max, 32, 0));
 }
 
+// Bytes of NUTS workspace this call needs (0: nothing to run, -1: unsupported shape).
+static int64_t nuts_need(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s) {
+  if (s->iter_end <= s->iter_begin || s->n_chains == 0) return 0;
+  // its Philox momenta drawn ahead (diagonal cov_p) for this call's iterations, or the tree vectors
+  // of the kernel this call takes
+  const int32_t pm = s->rng_mode == HMC_RNG_PHILOX && !k->minv_full ? 1 : 0;
+  const int64_t need = hmc_nuts_workspace_size_ex(t->D, s->n_chains, s->d_max, s->iter_end - s->iter_begin, pm);
+  return need > 0 ? need : -1;
+}
+
+hmc_status hmc_workspace_register(const void* workspace, int64_t bytes) {
+  if (!workspace || bytes < 0) return fail(HMC_EINVAL, "hmc_workspace_register: null pointer or negative size");
+  ws_record(workspace, bytes);
+  return HMC_OK;
+}
+
+hmc_status hmc_chain_init_ws(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, const hmc_replay* r,
+                             const double* q_start, hmc_state* st, int64_t order_bytes, void* stream) {
+  if (hmc_status e = check_schedule(t, k, s, false)) return e;
+  if (!st) return fail(HMC_EINVAL, "null state");
+  if (!k) return fail(HMC_EINVAL, "null kinetic");
+  const int64_t need = order_need(t, k, s, st);
+  if (order_bytes < need)
+    return fail(HMC_EINVAL, "hmc_chain_init_ws: state.order of %lld bytes, this call needs %lld "
+                "(hmc_random_workspace_size_ex)", (long long)order_bytes, (long long)need);
+  if (st->order) ws_record(st->order, order_bytes);
+  return hmc_chain_init(t, k, s, r, q_start, st, stream);
+}
+
+hmc_status hmc_random_iters_ws(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, const hmc_replay* r,
+                               hmc_state* st, int64_t order_bytes, void* stream) {
+  if (hmc_status e = check_schedule(t, k, s, true)) return e;
+  if (!st) return fail(HMC_EINVAL, "null state");
+  if (!k) return fail(HMC_EINVAL, "null kinetic");
+  const int64_t need = order_need(t, k, s, st);
+  if (order_bytes < need)
+    return fail(HMC_EINVAL, "hmc_random_iters_ws: state.order of %lld bytes, this call needs %lld "
+                "(hmc_random_workspace_size_ex)", (long long)order_bytes, (long long)need);
+  if (st->order) ws_record(st->order, order_bytes);
+  return hmc_random_iters(t, k, s, r, st, stream);
+}
+
 hmc_status hmc_nuts_iters_ws(const hmc_target* t, const hmc_kinetic* k, const hmc_schedule* s, const hmc_replay* r,
                              hmc_state* st, void* workspace, int64_t workspace_bytes, void* stream) {
-  if (hmc_status e = check_schedule(t, k, s, false)) return e;
+  if (hmc_status e = check_schedule(t, k, s, false)) return e;   // also rejects a NULL k
   if (s->d_max < 1 || s->d_max > hmc::kNutsDmaxMax) return fail(HMC_EINVAL, "d_max must be in [1, %d]", hmc::kNutsDmaxMax);
-  if (s->iter_end > s->iter_begin && s->n_chains > 0) {
-    // the sized workspace must cover this call: its Philox momenta drawn ahead (diagonal cov_p)
-    // for this call's iterations, or the tree vectors of the kernel this call takes
-    const int32_t pm = s->rng_mode == HMC_RNG_PHILOX && !k->minv_full ? 1 : 0;
-    const int64_t need = hmc_nuts_workspace_size_ex(t->D, s->n_chains, s->d_max, s->iter_end - s->iter_begin, pm);
-    if (need <= 0) return fail(HMC_EINVAL, "NUTS workspace: unsupported D=%d / d_max=%d", t->D, s->d_max);
-    if (workspace_bytes < need)
-      return fail(HMC_EINVAL, "NUTS workspace of %lld bytes; this call (D=%d, %lld chains, d_max=%d, %d iterations, "
-                  "%s momenta) needs %lld (hmc_nuts_workspace_size_ex)", (long long)workspace_bytes, t->D,
-                  (long long)s->n_chains, s->d_max, s->iter_end - s->iter_begin, pm ? "Philox" : "no pre-drawn",
-                  (long long)need);
-  }
+  const int64_t need = nuts_need(t, k, s);
+  if (need < 0) return fail(HMC_EINVAL, "NUTS workspace: unsupported D=%d / d_max=%d", t->D, s->d_max);
+  if (workspace_bytes < need)
+    return fail(HMC_EINVAL, "NUTS workspace of %lld bytes; this call (D=%d, %lld chains, d_max=%d, %d iterations, "
+                "%s momenta) needs %lld (hmc_nuts_workspace_size_ex)", (long long)workspace_bytes, t->D,
+                (long long)s->n_chains, s->d_max, s->iter_end - s->iter_begin,
+                s->rng_mode == HMC_RNG_PHILOX && !k->minv_full ? "Philox" : "no pre-drawn", (long long)need);
+  ws_record(workspace, workspace_bytes);
   return hmc_nuts_iters(t, k, s, r, st, workspace, stream);
 }
 
@@ -367,6 +440,11 @@ hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_s
   if (replay && (!r || !r->p || !r->tape || r->tape_stride < 1)) return fail(HMC_EINVAL, "replay mode needs p and tape");
   if (s->n_chains == 0 || s->iter_end == s->iter_begin) return HMC_OK;
   if (!workspace) return fail(HMC_EINVAL, "null workspace");
+  {
+    const int64_t need = nuts_need(t, k, s);
+    if (need < 0) return fail(HMC_EINVAL, "NUTS workspace: unsupported D=%d / d_max=%d", t->D, s->d_max);
+    if (hmc_status e = ws_check(workspace, need, "hmc_nuts_iters: workspace")) return e;
+  }
   const hmc::Layout lay{0, 0, 16, (t->D + 1) / 2};   // 16 chain slots per wave (debug stamps: one row per wave)
   hmc::RandArgs a = rand_args(t, k, s, replay ? r : nullptr, st, lay);
   a.d_max = s->d_max;

@@ -53,6 +53,12 @@ __device__ __forceinline__ uint32_t opaque_u32(uint32_t v) {
   asm volatile("" : "+v"(v));
   return v;
 }
+// A constant kept in an SGPR operand (the compiler would otherwise split the instruction that
+// reads it back into a shift and an or).
+__device__ __forceinline__ uint32_t opaque_s32(uint32_t v) {
+  asm("" : "+s"(v));
+  return v;
+}
 
 __device__ __forceinline__ uint4 draw_block(uint32_t slot, uint32_t iter, uint64_t gchain, uint32_t k0,
                                             uint32_t k1) {
@@ -67,7 +73,8 @@ __device__ __forceinline__ uint4 draw_block_uc(uint32_t slot, uint32_t iter, uin
   const uint32_t glo = (uint32_t)gchain, ghi = (uint32_t)(gchain >> 32);
   const uint64_t p0 = (uint64_t)slot * 0xD2511F53u;
   const uint64_t p1 = (uint64_t)glo * 0xCD9E8D57u;                      // uniform
-  uint4 c = make_uint4(iter ^ ((uint32_t)(p1 >> 32) ^ k0), (uint32_t)p1, (uint32_t)(p0 >> 32) ^ (ghi ^ k1),
+  // (ghi ^ k1) pinned in an SGPR: reassociated, the xor with the lane's word took two VALU
+  uint4 c = make_uint4(iter ^ ((uint32_t)(p1 >> 32) ^ k0), (uint32_t)p1, (uint32_t)(p0 >> 32) ^ opaque_s32(ghi ^ k1),
                        (uint32_t)p0);
   k0 += 0x9E3779B9u;
   k1 += 0xBB67AE85u;
@@ -172,10 +179,11 @@ __device__ __forceinline__ void fast_sincospi(double x, double& sn, double& cs) 
   cs = ((q + 1) & 2) ? -c0 : c0;
 }
 
-// [1, 2) with the top 52 bits of (hi:lo) as mantissa: 3 integer/bit VALU ops, no conversion.
+// [1, 2) with the top 52 bits of (hi:lo) as mantissa: two v_alignbit, no conversion.
 __device__ __forceinline__ double one_to_two(uint32_t lo, uint32_t hi) {
   const uint32_t mlo = __builtin_amdgcn_alignbit(hi, lo, 12);   // low word of (hi:lo) >> 12
-  const uint32_t mhi = (hi >> 12) | 0x3FF00000u;
+  // (0x3FF:hi) >> 12 = (hi >> 12) | 0x3FF00000, the exponent of [1, 2) shifted in with the bits
+  const uint32_t mhi = __builtin_amdgcn_alignbit(opaque_s32(0x3FFu), hi, 12);
   return __builtin_bit_cast(double, ((uint64_t)mhi << 32) | mlo);
 }
 
@@ -230,18 +238,21 @@ __device__ __forceinline__ double table_log(double u, const double* tab) {
   const int k = __builtin_amdgcn_frexp_exp(u);
   const double m = __builtin_amdgcn_frexp_mant(u);
   const uint32_t mhi = (uint32_t)(__builtin_bit_cast(uint64_t, m) >> 32);
-  const int j = (int)((mhi >> kLogShift) & (kLogN - 1));
-  const double2 e = lds_pair(tab + 2 * kTrigN + 2 * j);
+  // byte offset 16 j of bucket j = (mhi >> kLogShift) & (kLogN - 1): one shift, one and
+  const uint32_t j16 = (mhi >> (kLogShift - 4)) & ((kLogN - 1) << 4);
+  const double2 e = lds_pair(reinterpret_cast<const double*>(reinterpret_cast<const char*>(tab + 2 * kTrigN) + j16));
   const double r = __builtin_fma(m, e.x, -1.0);
 #ifdef HMC_SMALL_TABLES
   double pl = fmac_k(r, 1.0 / 7.0, -1.0 / 6.0);
   pl = fmac_k(r, pl, 1.0 / 5.0);
   pl = fmac_k(r, pl, -1.0 / 4.0);
 #else
+  // (an output-modifier form, (0.4 r - 0.5) with div:2, measured wrong on gfx950: omod is not
+  // applied to this f64 FMA; test_table_normals_match_kernel caught it)
   double pl = fmac_k(r, 1.0 / 5.0, -1.0 / 4.0);
 #endif
   pl = fmac_k(r, pl, 1.0 / 3.0);
-  pl = fmac_k(r, pl, -0.5);
+  pl = __builtin_fma(r, pl, -0.5);                                      // inline constant
   const double l1p = __builtin_fma(r * r, pl, r);                       // log1p(r)
   const double dk = (double)k;
   return __builtin_fma(dk, 6.93147180369123816490e-01, e.y + __builtin_fma(dk, 1.90821492927058770002e-10, l1p));
@@ -253,9 +264,11 @@ __device__ __forceinline__ double table_log(double u, const double* tab) {
 __device__ __forceinline__ void table_cossin(double d, const double* tab, double& cs, double& sn) {
   const uint64_t bits = __builtin_bit_cast(uint64_t, d);
   const uint32_t hi = (uint32_t)(bits >> 32);
-  const int i = (int)((hi >> kTrigShift) & (kTrigN - 1));
+  const uint32_t i16 = (hi >> (kTrigShift - 4)) & ((kTrigN - 1) << 4);   // byte offset of entry i
   const double f = __builtin_bit_cast(double, bits & ~((uint64_t)(kTrigN - 1) << (32 + kTrigShift))) - 1.0;  // exact
-  const double dl = __builtin_fma(f, 6.28318530717958623200e+00, f * 2.44929359829470635445e-16);
+  // delta = 2 pi f rounded once: delta < 2 pi / 1024, so the low part of 2 pi (2.4e-16 relative)
+  // would move the final (cos, sin) by < 1e-19, far below their ulp
+  const double dl = f * 6.28318530717958623200e+00;
   const double z = dl * dl;
 #ifdef HMC_SMALL_TABLES
   double ps = fmac_k(z, -1.0 / 5040.0, 1.0 / 120.0);
@@ -267,20 +280,35 @@ __device__ __forceinline__ void table_cossin(double d, const double* tab, double
 #else
   const double ps = fmac_k(z, 1.0 / 120.0, -1.0 / 6.0);
   const double sd = __builtin_fma(dl * z, ps, dl);                       // sin(delta)
-  double pc = fmac_k(z, -1.0 / 720.0, 1.0 / 24.0);
-  pc = fmac_k(z, pc, -0.5);
+  // cos to delta^4: delta^6/720 < 7.5e-17 < ulp(1)/2 for delta < 2 pi/1024
+  double pc;
+  asm("v_fma_f64 %0, %1, %2, -0.5" : "=v"(pc) : "v"(z), "s"(1.0 / 24.0));
 #endif
   const double cd = __builtin_fma(z, pc, 1.0);                          // cos(delta)
-  const double2 t = lds_pair(tab + 2 * i);                              // (cos, sin)(theta_i)
+  const double2 t = lds_pair(reinterpret_cast<const double*>(reinterpret_cast<const char*>(tab) + i16));  // (cos, sin)(theta_i)
   cs = __builtin_fma(t.x, cd, -(t.y * sd));
   sn = __builtin_fma(t.y, cd, t.x * sd);
 }
 
 // Two independent N(0,1) from one Philox block, table-driven Box–Muller (same uniforms as
 // normal_pair: u1 = 2 - d1 in (0, 1], angle 2*pi*(d2 - 1)).
+// sqrt(t) for the Box-Muller radius: t = -2 log u1 >= 0 up to the table log's rounding at u1 = 1
+// (probability 2^-52), so one v_max against a tiny floor replaces fast_sqrt's zero test and its
+// two selects (radius 2^-500 instead of 0 there).
+__device__ __forceinline__ double bm_sqrt(double t) {
+  t = __builtin_fmax(t, 0x1p-1000);
+  const double y = __builtin_amdgcn_rsq(t);
+  double g = t * y, h = 0.5 * y;
+  const double r = __builtin_fma(-g, h, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  const double d = __builtin_fma(-g, g, t);
+  return __builtin_fma(d, h, g);
+}
+
 __device__ __forceinline__ void normal_pair_tab(uint4 r, const double* tab, double& z0, double& z1) {
   const double u1 = 2.0 - one_to_two(r.x, r.y);
-  const double rad = fast_sqrt(-2.0 * table_log(u1, tab));
+  const double rad = bm_sqrt(-2.0 * table_log(u1, tab));
   double c, s;
   table_cossin(one_to_two(r.z, r.w), tab, c, s);
   z0 = rad * c;
@@ -385,6 +413,23 @@ __device__ __forceinline__ double wave_sum_dpp_l63(double v) {
 
 __device__ __forceinline__ double wave_sum_dpp(double v) { return readlane_d(wave_sum_dpp_l63(v), 63); }
 
+// Two full-wave sums for the price of one (18 VALU instead of 36): one v_permlane32_swap per
+// 32-bit half puts lanes 0-31 of `a` and of `b` side by side (and lanes 32-63 in the other
+// result), so one add leaves a's pair sums in lanes 0-31 and b's in lanes 32-63; the row_shr
+// prefix steps and one row_bcast:15 (into rows 1 and 3 only) then finish both halves at once.
+// Lane 31 holds sum(a), lane 63 holds sum(b); other lanes hold partial sums.  EXEC all ones.
+__device__ __forceinline__ double wave_sum2_dpp(double a, double b) {
+  const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(a), __double2loint(b), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(a), __double2hiint(b), false, false);
+  double v = __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+  v += dpp_u<0x111>(v);        // row_shr:1
+  v += dpp_u<0x112>(v);        // row_shr:2
+  v += dpp_u<0x114>(v);        // row_shr:4
+  v += dpp_u<0x118>(v);        // row_shr:8
+  v += dpp_u<0x142, 0xA>(v);   // row_bcast:15 -> rows 1, 3
+  return v;
+}
+
 // Lane 63's bit of a compare mask as a wave-uniform bool (EXEC must be all ones): the sign of the
 // mask's bit 63, tested on the SALU (written in C the compiler emits a VALU 64-bit compare of the
 // SGPR pair for it and for its negation).
@@ -392,6 +437,13 @@ __device__ __forceinline__ bool lane63(uint64_t mask) {
   int r;
   asm("s_bitcmp1_b64 %1, 63\n\ts_cselect_b32 %0, 1, 0" : "=s"(r) : "s"(mask) : "scc");
   return r != 0;
+}
+// Lane 31's bit (where wave_sum2_dpp leaves its first sum) as 0/1 in an SGPR, on the SALU as
+// lane63 (callers count it with scalar adds: a C bool -> int conversion compiles to v_cndmask).
+__device__ __forceinline__ uint32_t lane31(uint64_t mask) {
+  uint32_t r;
+  asm("s_bitcmp1_b64 %1, 31\n\ts_cselect_b32 %0, 1, 0" : "=s"(r) : "s"(mask) : "scc");
+  return r;
 }
 
 // Parks v (valid in lane 63, where a DPP reduction leaves its total) in lane n of buf: two
@@ -414,6 +466,13 @@ __device__ __forceinline__ double park_lane(double buf, double v, int n, int bp6
 }
 
 __device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// (a < b) as 0/1 in an SGPR for wave-uniform a, b (the C form goes through v_cndmask + readfirstlane).
+__device__ __forceinline__ uint32_t s_lt_i32(int a, int b) {
+  uint32_t r;
+  asm("s_cmp_lt_i32 %1, %2\n\ts_cselect_b32 %0, 1, 0" : "=s"(r) : "s"(a), "s"(b) : "scc");
+  return r;
+}
 
 // Wave-uniform max of an int: DPP row_shr 1/2/4/8 then row_bcast 15/31 (each step one VALU max
 // with the DPP source; lanes without a source keep their value), lane 63 read back.

@@ -133,8 +133,9 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
   constexpr bool RING = K == 1 && !REPLAY;
 #endif
   __shared__ double s_ntab[REPLAY ? 2 : kNormalTableDoubles];   // Box–Muller tables (Philox mode)
-  // per wave: kRingPairs ring slots + one zero pair that lanes past npairs read (p = 0 there)
-  __shared__ double s_ring[RING ? (kK1Block / kWave) * 2 * (kRingPairs + 1) : 2];
+  // per wave: kRingPairs ring slots (2 KB, 2 KB-aligned: a slot's byte address is the wave's base
+  // OR'd with 16 * slot)
+  __shared__ __attribute__((aligned(2048))) double s_ring[RING ? (kK1Block / kWave) * 2 * kRingPairs : 2];
   if constexpr (!REPLAY) {
     init_normal_tables(s_ntab);
     __syncthreads();
@@ -143,16 +144,16 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
   const int64_t c = uniform_i(blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave));
   if (c >= a.n) return;                                  // whole wave, uniform
   const uint64_t gc = (uint64_t)(a.chain_offset + c);
-  double* const ring = s_ring + (RING ? (threadIdx.x / kWave) * 2 * (kRingPairs + 1) : 0);
-  if constexpr (RING) {
-    if (lane == 0) *reinterpret_cast<double2*>(ring + 2 * kRingPairs) = make_double2(0.0, 0.0);
-  }
+  const uint32_t ring_off = RING ? (threadIdx.x / kWave) * (16 * kRingPairs) : 0;   // bytes, 2 KB multiple
+  char* const ring_b = reinterpret_cast<char*>(s_ring);
+  char* const ring_lane = ring_b + ring_off + 16 * lane;   // this lane's slot in a pass's half
   // Generator position: pairs drawn so far (wave-uniform) and this lane's (pair, iteration) for the
   // next pass.  npairs is in (32, 64] for the wave kernel, so one pass of 64 pairs advances a lane
   // by one or two whole iterations: the position is kept incrementally instead of re-derived.
   int gen_n = 0;
-  int gk = lane, git = a.it0;
-  if (gk >= a.npairs) { gk -= a.npairs; ++git; }
+  uint32_t gk = lane, git = a.it0;
+  if (gk >= (uint32_t)a.npairs) { gk -= a.npairs; ++git; }
+  const uint32_t gadv = kWave - a.npairs;                // uniform: a pass moves a lane 64 pairs on
   // momentum of iteration `it` through the ring: at most one 64-pair pass is due (the pairs drawn
   // so far cover every earlier iteration and npairs <= 64), and the ring never holds more than
   // npairs + 64 <= kRingPairs pairs that are not consumed yet
@@ -160,25 +161,35 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     const int base = (it - a.it0) * a.npairs;
     if (gen_n < base + a.npairs) {                       // wave-uniform
       double z0, z1;
-      normal_pair_tab(draw_block_uc((uint32_t)gk, (uint32_t)git, gc, a.k0, a.k1), s_ntab, z0, z1);
-      if constexpr (ODD) z1 = gk == a.npairs - 1 ? 0.0 : z1;   // dimension D does not exist
-      *reinterpret_cast<double2*>(ring + 2 * ((gen_n + lane) & (kRingPairs - 1))) = make_double2(z0, z1);
+      normal_pair_tab(draw_block_uc(gk, git, gc, a.k0, a.k1), s_ntab, z0, z1);
+      if constexpr (ODD) z1 = gk == (uint32_t)a.npairs - 1 ? 0.0 : z1;   // dimension D does not exist
+      // pass slots gen_n + lane (mod 128) = lane + (gen_n & 64): gen_n is a multiple of 64
+      *reinterpret_cast<double2*>(ring_lane + 16 * (gen_n & kWave)) = make_double2(z0, z1);
       __builtin_amdgcn_wave_barrier();
       gen_n += kWave;
-      gk += kWave - a.npairs;                            // >= 0: one wrap always happens
-      const int wrap = gk >= a.npairs ? 1 : 0;           // and at most one more
-      git += 1 + wrap;
-      gk -= wrap * a.npairs;
+      // next pass: gk += 64 - npairs, then one more wrap (git + 2) or none (git + 1); four VALU:
+      // the borrow of gk - npairs picks both the new gk and git's increment
+      uint64_t bo;
+      uint32_t t;
+      asm("v_add_u32_e32 %0, %4, %0\n\t"
+          "v_subrev_co_u32_e32 %2, vcc, %5, %0\n\t"
+          "v_subb_co_u32_e64 %1, %3, %1, -2, vcc\n\t"
+          "v_cndmask_b32_e32 %0, %2, %0, vcc"
+          : "+v"(gk), "+v"(git), "=&v"(t), "=&s"(bo)
+          : "s"(gadv), "s"(a.npairs)
+          : "vcc");
     }
-    // lanes past npairs read the zero pair: p = 0 in the padding without a branch
-    const int slot = lane < a.npairs ? ((base + lane) & (kRingPairs - 1)) : kRingPairs;
-    const double2 z = *reinterpret_cast<const double2*>(ring + 2 * slot);
-    pp[0] = z.x;
-    pp[1] = z.y;
-    if (GEN && a.pscale && lane < a.npairs) {
-      const int d = 2 * lane;
-      pp[0] *= a.pscale[d];
-      if (d + 1 < a.D) pp[1] *= a.pscale[d + 1];
+    // lanes past npairs sit the read out (EXEC off): their p is never written and stays 0
+    if (lane < a.npairs) {
+      const uint32_t slot_b = (((uint32_t)(base + lane) << 4) & (16 * kRingPairs - 1)) | ring_off;
+      const double2 z = *reinterpret_cast<const double2*>(ring_b + slot_b);
+      pp[0] = z.x;
+      pp[1] = z.y;
+      if (GEN && a.pscale) {
+        const int d = 2 * lane;
+        pp[0] *= a.pscale[d];
+        if (d + 1 < a.D) pp[1] *= a.pscale[d + 1];
+      }
     }
   };
   // the ring (Philox, K = 1) kernels are specialised on the parity of D: `even` is then a
@@ -193,6 +204,8 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     kk[j] = lane + kWave * j;
     pv[j] = kk[j] < a.npairs;
     q[2 * j] = q[2 * j + 1] = 0.0;
+    p[2 * j] = p[2 * j + 1] = 0.0;      // the ring leaves lanes past npairs at p = 0
+    pn[2 * j] = pn[2 * j + 1] = 0.0;
     if (pv[j]) load_pair(qrow, kk[j], even, 2 * kk[j] + 1 < a.D, q[2 * j], q[2 * j + 1]);
   }
   double Eprev = a.Eprev[c];
@@ -202,13 +215,19 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
   if constexpr (RING) ring_momentum(a.it0, p);
   else wave_momentum<K, GEN, REPLAY>(a, c, gc, a.it0, kk, pv, p, s_ntab);
   // FASTID: FAST integrator on an identity-precision target (the headline instantiation): FMA
-  // energy partials, E = fma(sum, 1/2, logc/2), Metropolis test finished in lane 63
+  // energy partials and ONE reduction per iteration.  The lane's part of 2 E0 - logc (e0l, known
+  // when the iteration starts) and of 2 (E1 - E0) (its q.q + p.p after the leapfrog minus e0l)
+  // are summed together by wave_sum2_dpp: lane 31 holds 2 dE for the Metropolis test, lane 63
+  // 2 E0 - logc for E_chain.  E = fma(sum, 1/2, logc/2); dE is summed directly (no cancellation
+  // of two ~D-sized energies), which FAST mode's 1e-10 contract allows.
   constexpr bool FASTID = !EXACT && !GEN;
   const double hlogc = 0.5 * a.logc;
   double m0, k0, m0l;   // m0l: this lane's part of the potential of q (FAST mode bookkeeping)
+  double e0l = 0.0;     // FASTID: this lane's part of q.q + p.p at the iteration start
   if constexpr (FASTID) {
-    wave_partials_fma<K>(q, p, m0l, k0);
+    wave_partials_fma<K>(q, p, m0l, e0l);
     m0 = m0l;
+    k0 = 0.0;
   } else {
     wave_partials<K, GEN>(a, kk, pv, q, p, m0, k0);
     m0l = m0;
@@ -219,8 +238,8 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
   } else if constexpr (!FASTID) {   // one reduction of V + K
     k0 = wave_sum_dpp(m0 + k0);
   }
-  double E0 = EXACT ? 0.5 * (a.logc + (m0 + k0))
-                    : (FASTID ? __builtin_fma(wave_sum_dpp_l63(k0), 0.5, hlogc) : 0.5 * (a.logc + k0));
+  // (FASTID: E0 of an iteration is formed inside it, by that iteration's one reduction)
+  double E0 = EXACT ? 0.5 * (a.logc + (m0 + k0)) : (FASTID ? 0.0 : 0.5 * (a.logc + k0));
 
   // thinning bookkeeping without divisions: row = (it - wu)//thin, phase = (it - wu) % thin
   int row = 0, phase = 0;
@@ -229,7 +248,7 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     phase = (a.it0 - a.wu) - row * a.thin;
   }
   int qslot = row % a.Lq;                                // q_chain buffer row of `row` (circular window)
-  double Ebuf = 0.0, dEbuf = 0.0, Eprev_first = 0.0;
+  double Ebuf = 0.0, dEbuf = 0.0;
   int row_first = 0, nbuf = 0;
   const bool thin1 = a.thin == 1;
   const int bp63 = (int)opaque_u32((kWave - 1) * 4);     // park_lane's source lane (byte address)
@@ -240,7 +259,7 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     double dE = dEbuf;
     if (thin1) {
       const double before = __shfl_up(Ebuf, 1, kWave);
-      dE = Ebuf - (lane == 0 ? readlane_d(Eprev_first, kWave - 1) : before);
+      dE = lane == 0 ? dEbuf : Ebuf - before;   // lane 0: parked when the block began
     }
     if (lane < n) {
       if (Ec) __builtin_nontemporal_store(Ebuf, Ec + row_first + lane);
@@ -268,26 +287,35 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     // Eprev (the E of the previous iteration) is only needed for a block's first row when
     // thin = 1: it is then refreshed at each flush instead of every iteration.
     // (the empty asm statements keep these uniform conditions as branches, not per-lane selects)
-    if (write_row) {
-      if (nbuf == 0) {
-        asm volatile("" ::: "memory");
-        row_first = row;
-        Eprev_first = Eprev;
+    // FASTID parks after the iteration's reduction has formed E0; the other modes know E0 here.
+    auto park_row = [&]() {
+      if (write_row) {
+        if (nbuf == 0) {
+          asm volatile("" ::: "memory");
+          row_first = row;
+          // thin = 1: the block's first dE (its E minus the E before the block) in lane 0 of
+          // dEbuf; the flush forms the others from consecutive parked E
+          if (thin1) dEbuf = park_lane(dEbuf, E0 - Eprev, 0, bp63);
+        }
+        Ebuf = park_lane(Ebuf, E0, nbuf, bp63);
+        if (!thin1) {
+          asm volatile("" ::: "memory");
+          dEbuf = park_lane(dEbuf, E0 - Eprev, nbuf, bp63);
+        }
+        if (++nbuf == kWave) {
+          flush_E(kWave);
+          nbuf = 0;
+          if (thin1) Eprev = E0;
+        }
+        if (!thin1) {
+          asm volatile("" ::: "memory");
+          Eprev = E0;
+        }
+      } else {
+        Eprev = E0;
       }
-      Ebuf = park_lane(Ebuf, E0, nbuf, bp63);
-      if (!thin1) {
-        asm volatile("" ::: "memory");
-        dEbuf = park_lane(dEbuf, E0 - Eprev, nbuf, bp63);
-      }
-      if (++nbuf == kWave) {
-        flush_E(kWave);
-        nbuf = 0;
-        if (thin1) Eprev = E0;
-      }
-      if (!thin1) Eprev = E0;
-    } else {
-      Eprev = E0;
-    }
+    };
+    if constexpr (!FASTID) park_row();
 
     // trajectory length (:441) and MH log-uniform (:461): wave-uniform
     int L;
@@ -295,6 +323,7 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     if constexpr (REPLAY) {
       L = a.rL[c * (int64_t)a.niter + (it - 1)];
       lnu = a.rlnu[c * (int64_t)a.niter + (it - 1)];
+      if constexpr (FASTID) lnu *= 2.0;                  // compared with 2 dE (exact scaling)
     } else {
       if (it - it_base >= kWave) {                       // lane l draws (L, u) of iteration it + l
         it_base = it;
@@ -302,6 +331,7 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
         draw_L = uniform_int(r.x, a.L_low, a.L_high);
         const double u = u53(r.z, r.w);
         draw_lnu = u > 0.0 ? fast_log(u) : -__builtin_inf();   // log(random()), :461
+        if constexpr (FASTID) draw_lnu *= 2.0;           // compared with 2 dE (exact scaling)
       }
       L = __builtin_amdgcn_readlane(draw_L, it - it_base);
       lnu = readlane_d(draw_lnu, it - it_base);
@@ -402,13 +432,15 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
       }
     }
 
-    // FASTID: E1's partials and DPP chain first; p is then dead, so the next momentum is drawn
-    // into p itself (no copy at the end of the iteration)
-    double m1 = 0.0, k1 = 0.0, m1l = 0.0, s1 = 0.0;
+    // FASTID: E1's partials and the iteration's one reduction first; p is then dead, so the next
+    // momentum is drawn into p itself (no copy at the end of the iteration)
+    double m1 = 0.0, k1 = 0.0, m1l = 0.0, s2 = 0.0;
     if constexpr (FASTID) {
       wave_partials_fma<K>(q, p, m1l, k1);
       m1 = m1l;
-      s1 = wave_sum_dpp_l63(k1);
+      s2 = wave_sum2_dpp(k1 - e0l, e0l);   // lane 31: 2 (E1 - E0); lane 63: 2 E0 - logc
+      E0 = __builtin_fma(s2, 0.5, hlogc);  // E0 of this iteration (lane 63)
+      park_row();
     }
     // next iteration's momentum (keyed by it+1) so its kinetic energy joins this reduction
     const bool more = it + 1 < a.it1;
@@ -417,24 +449,15 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
     if (more && !(FULL && (a.dbg & 256))) {
       if constexpr (RING) ring_momentum(it + 1, pnext);
       else wave_momentum<K, GEN, REPLAY>(a, c, gc, it + 1, kk, pv, pnext, s_ntab);
-      if constexpr (FASTID) {
-        kn = pnext[1] * pnext[1];
-        kn = __builtin_fma(pnext[0], pnext[0], kn);
-#pragma unroll
-        for (int e = 2; e < 2 * K; ++e) kn = __builtin_fma(pnext[e], pnext[e], kn);
-      } else {
-        kn = kin_partial<K, GEN>(a, kk, pv, pnext);
-      }
+      if constexpr (!FASTID) kn = kin_partial<K, GEN>(a, kk, pv, pnext);
     }
     bool accept;
+    uint32_t acc1 = 0;   // accept as 0/1 in an SGPR (FASTID), for the tallies
     if constexpr (FASTID) {
-      // E1 - E0 and the test in lane 63, where the DPP chain leaves the total (samplers.py:459-462)
-      const double dE = __builtin_fma(s1, 0.5, hlogc) - E0;
-#ifdef HMC_AB_SELECT
-      accept = __builtin_amdgcn_ballot_w64((dE < 0.0) || (lnu < -dE)) >> 63;
-#else
-      accept = lane63(__builtin_amdgcn_ballot_w64(dE < 0.0) | __builtin_amdgcn_ballot_w64(lnu < -dE));
-#endif
+      // the test in lane 31 (samplers.py:459-462): dE < 0  <=>  2 dE < 0, and
+      // log u < -dE  <=>  2 log u < -2 dE (lnu holds 2 log u here; both scalings are exact)
+      acc1 = lane31(__builtin_amdgcn_ballot_w64(s2 < 0.0) | __builtin_amdgcn_ballot_w64(lnu < -s2));
+      accept = acc1 != 0;
     } else {
       wave_partials<K, GEN>(a, kk, pv, q, p, m1, k1);
       m1l = m1;
@@ -466,16 +489,27 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
       a.traj_len[it - 1] = (L > 0 ? L : 0) + 1;
       a.decision[it - 1] = accept ? 1 : 0;
     }
-    if (accept) {
-      if (post) ++n_acc; else ++n_acc_wu;
-    } else if (it < a.i_oob) {
-      ++n_oob;
-    }
+    // tallies as scalar adds of the (uniform) decision: as `if (accept) ++n` the compiler merged
+    // the increments through a pointer select and kept the counters in scratch (a load, a
+    // vmcnt(0) wait behind the row store, and a store per iteration)
+    if constexpr (!FASTID) acc1 = accept ? 1u : 0u;
+    if (post) n_acc += acc1; else n_acc_wu += acc1;
+    n_oob += (acc1 ^ 1u) & s_lt_i32(it, a.i_oob);
     const uint32_t Lp = L > 0 ? (uint32_t)L : 0u;
     n_lf += Lp;
     n_lf2 += Lp * Lp;
-    // advance
-    if (more) {
+    // advance (FASTID: the next e0l unconditionally, so the one this iteration reduced is dead
+    // after the reduction and the permlane swap may take its register)
+    if constexpr (FASTID) {
+      if (accept) {
+        asm volatile("" ::: "memory");
+        m0l = m1l;
+      }
+      e0l = __builtin_fma(p[1], p[1], m0l);   // V + K partial of the next iteration's start
+      e0l = __builtin_fma(p[0], p[0], e0l);
+#pragma unroll
+      for (int e = 2; e < 2 * K; ++e) e0l = __builtin_fma(p[e], p[e], e0l);
+    } else if (more) {
       if constexpr (!FASTID) {
 #pragma unroll
         for (int e = 0; e < 2 * K; ++e) p[e] = pn[e];
@@ -490,9 +524,7 @@ __device__ __forceinline__ void wave_iters(const RandArgs& a) {
 #endif
           m0l = m1l;
         }
-        // FASTID: E0 stays in lane 63 (the test, the park and Eprev read it there)
-        E0 = FASTID ? __builtin_fma(wave_sum_dpp_l63(m0l + kn), 0.5, hlogc)
-                    : 0.5 * (a.logc + wave_sum_dpp(m0l + kn));
+        E0 = 0.5 * (a.logc + wave_sum_dpp(m0l + kn));
       }
     }
     if (post && ++phase == a.thin) {
@@ -576,6 +608,13 @@ hipError_t launch_wave_k(const RandArgs& a, bool exact, bool gen, bool replay, d
 }  // namespace
 
 hipError_t launch_wave_iters(const RandArgs& a, int K, bool exact, bool gen, bool replay, hipStream_t s) {
+#ifdef HMC_WAVE_PROD_ONLY   // dev: ISA inspection of the headline instance only (seconds to compile)
+  if (K == 1 && !exact && !gen && !replay) {
+    launch_wave_one<1, false, false, false>(a, dim3(1), s);
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
+#endif
   const dim3 grid((unsigned)((a.n + 3) / 4));
   switch (K) {
     case 1: return launch_wave_k<1>(a, exact, gen, replay, grid, s);

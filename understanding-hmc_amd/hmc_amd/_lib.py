@@ -59,6 +59,12 @@ SYMBOLS = {
                                       ctypes.POINTER(Replay), c_dp, ctypes.POINTER(State), c_dp]),
     "hmc_random_iters": (ctypes.c_int, [ctypes.POINTER(Target), ctypes.POINTER(Kinetic), ctypes.POINTER(Schedule),
                                         ctypes.POINTER(Replay), ctypes.POINTER(State), c_dp]),
+    "hmc_chain_init_ws": (ctypes.c_int, [ctypes.POINTER(Target), ctypes.POINTER(Kinetic), ctypes.POINTER(Schedule),
+                                         ctypes.POINTER(Replay), c_dp, ctypes.POINTER(State), ctypes.c_int64, c_dp]),
+    "hmc_random_iters_ws": (ctypes.c_int, [ctypes.POINTER(Target), ctypes.POINTER(Kinetic),
+                                           ctypes.POINTER(Schedule), ctypes.POINTER(Replay), ctypes.POINTER(State),
+                                           ctypes.c_int64, c_dp]),
+    "hmc_workspace_register": (ctypes.c_int, [c_dp, ctypes.c_int64]),
     "hmc_stream_work_size": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
     "hmc_stream_accumulate": (ctypes.c_int, [c_dp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
                                              ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,

@@ -428,6 +428,7 @@ class StreamingDiagnostics:
         self._z = lambda *s: torch.zeros(s, dtype=torch.float64, device=dev)  # noqa: E731
         self.pos = 0                                                    # samples consumed
         self.mode = mode                                                # "exact" | "stream"; None: the feeder picks
+        self.window_rows = None                                         # rows of the feeder's window (first call)
         self._stream_state = None
         self.halves = []                                                # exact: halves added, in order
         self.xsums = None                                               # exact: sums about xshift

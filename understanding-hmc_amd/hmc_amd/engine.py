@@ -101,6 +101,7 @@ class RandomEngine:
         else:
             nbytes = 0
         self._order = torch.zeros((nbytes + 3) // 4, dtype=torch.int32, device=dev) if nbytes > 0 else None
+        self._order_bytes = self._order.numel() * 4 if self._order is not None else 0
         self.S.order = H.ptr(self._order)
         self._replay = None
         self._streams = []
@@ -141,13 +142,13 @@ class RandomEngine:
         qs = q_start if isinstance(q_start, torch.Tensor) else _dev(np.asarray(q_start).reshape(self.N, self.D),
                                                                     self.device)
         self._qs = qs.to(self.device, torch.float64).contiguous()
-        H.check(H.lib().hmc_chain_init(self.T, self.K, self.schedule(1, 1), self._replay, H.ptr(self._qs), self.S,
-                                       self.stream()), "hmc_chain_init")
+        H.check(H.lib().hmc_chain_init_ws(self.T, self.K, self.schedule(1, 1), self._replay, H.ptr(self._qs), self.S,
+                                          self._order_bytes, self.stream()), "hmc_chain_init")
 
     def run(self, it0, it1):
         """Iterations [it0, it1) of every chain in ONE fused kernel launch."""
-        H.check(H.lib().hmc_random_iters(self.T, self.K, self.schedule(it0, it1), self._replay, self.S,
-                                         self.stream()), "hmc_random_iters")
+        H.check(H.lib().hmc_random_iters_ws(self.T, self.K, self.schedule(it0, it1), self._replay, self.S,
+                                            self._order_bytes, self.stream()), "hmc_random_iters")
 
     def run_streaming(self, diag, it_begin, it_end, step, events=None, feed=None):
         """Iterations [it_begin, it_end) in launches of `step`, with q_chain rows kept only in a
@@ -177,12 +178,17 @@ class RandomEngine:
             W = W2 if W2 <= W_seg else diag.n + -(-step // self.thin) + 2
         else:
             W = W_seg
+        # the mode and the window size are decided by the first call and recorded in `diag` (and
+        # so in a checkpoint): a later call, or a resumed run, with another step or feed would
+        # otherwise pick another mode or window size, and rows already written (the open half, the
+        # variogram carry) would be silently replaced by a zeroed window (advisor r05)
+        if diag.mode is None:
+            diag._set_mode("exact" if exact else "stream")
+        if diag.window_rows is not None and diag.window_rows != W:
+            raise AssertionError("run_streaming continued with step/feed giving a %d-row window; the "
+                                 "statistics' window has %d rows (use the same step and feed)" % (W, diag.window_rows))
+        diag.window_rows = W
         st = getattr(self, "_stream", None)
-        if st is not None and st[0] is diag and st[1].shape[1] != W and diag.pos > 0:
-            # the window holds the variogram carry (and possibly written but unfed rows) at
-            # slots r % W_old: a different W would silently drop them
-            raise AssertionError("run_streaming resumed with step/feed giving a %d-row window; the "
-                                 "statistics' window has %d rows (use the same step and feed)" % (W, st[1].shape[1]))
         if st is None or st[0] is not diag or st[1].shape[1] != W:
             st = [diag, torch.zeros((N, W, D), dtype=torch.float64, device=self.device)]
             self._stream = st
@@ -253,6 +259,7 @@ class RandomEngine:
                 arr["window"] = st[1]                       # rows of an open half / the lag carry
         meta = dict(self._meta(), it_next=int(it_next), diag_pos=None if diag is None else diag.pos,
                     diag_mode=None if diag is None else diag.mode,
+                    diag_window_rows=None if diag is None else diag.window_rows,
                     diag_halves=None if diag is None else list(diag.halves))
         np.savez(path, meta=np.array(json.dumps(meta)), **{k: v.cpu().numpy() for k, v in arr.items()})
 
@@ -274,6 +281,7 @@ class RandomEngine:
                 self._order.zero_()                         # no cached gradient: recomputed from q
             if diag is not None:
                 diag.mode = meta.get("diag_mode")
+                diag.window_rows = meta.get("diag_window_rows")
                 diag.halves = list(meta.get("diag_halves") or [])
                 if diag.mode == "exact":
                     if "diag_xsums" in z.files:
