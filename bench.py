@@ -83,6 +83,9 @@ def parse(argv=None):
     ap.add_argument("--sampler", default="random", choices=["random", "nuts"],
                     help="nuts: BASELINE config 5 (use with --rho 0.95 --chains 65536)")
     ap.add_argument("--d-max", type=int, default=10)
+    ap.add_argument("--cov-p-rho", type=float, default=0.0,
+                    help="nuts: a full (non-diagonal) cov_p with this correlation (samplers.py:352-356; a "
+                         "shape-range line, 6D^2 + 12D flops per leapfrog: P x, the kick inv_cov_p.P x, K)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget per process")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ess", action="store_true", help="no q_chain rows at all (ablation; not a metric line)")
@@ -387,9 +390,12 @@ def main():
     R = window_rows(timed_rows, int(a.chain_budget_gb * 1e9 // (8.0 * max(1, ref_chains) * D))) if store else 0
     cov = np.eye(D) if a.rho == 0 else (np.diag(np.ones(D)) * (1 - a.rho) + a.rho)
     tgt = MVNTarget(np.zeros(D), cov)
+    mass = nuts and a.cov_p_rho != 0
     if nuts:
-        eng = NutsEngine(tgt, N, n_iter, wu, 1, a.d_max, a.dt, rng="philox", seed=a.seed, fp_mode=a.fp_mode,
-                         chain_offset=offset, store_chain=False, on_dmax="break", device=dev, iters_per_call=S)
+        cov_p = (np.diag(np.ones(D)) * (1 - a.cov_p_rho) + a.cov_p_rho) if mass else None
+        eng = NutsEngine(tgt, N, n_iter, wu, 1, a.d_max, a.dt, cov_p=cov_p, rng="philox", seed=a.seed,
+                         fp_mode=a.fp_mode, chain_offset=offset, store_chain=False, on_dmax="break", device=dev,
+                         iters_per_call=S)
     else:
         eng = RandomEngine(tgt, N, n_iter, wu, 1, 5, 20, a.dt, rng="philox", seed=a.seed, fp_mode=a.fp_mode,
                            chain_offset=offset, store_chain=False, device=dev, order_tiles=not a.no_order_tiles)
@@ -500,7 +506,8 @@ def main():
         row_bytes = 8 * D if (store or sd is not None) else 0
         bytes_moved = N * (S * (row_bytes + 16) + dispatches * (16 * D + 16))
         if dense:   # 2D^2 + 7D per leapfrog (Random dense), 2D^2 + 12D (NUTS: E + U-turn dots)
-            flops_launch = lf_launch * (2 * D * D + (12 if nuts else 7) * D)
+            # (a full cov_p: + 2D^2 for the kick inv_cov_p.(P x) and 2D^2 for K = p.inv_cov_p.p)
+            flops_launch = lf_launch * ((6 if mass else 2) * D * D + (12 if nuts else 7) * D)
         else:       # 8D per leapfrog + 8D energies per iteration
             flops_launch = lf_launch * 8 * D + N * S * 8 * D
         kern_s = kern_ms / 1e3
@@ -509,6 +516,8 @@ def main():
         kname = "hmc_nuts_iters" if nuts else ("hmc_random_iters(dense)" if dense else "hmc_random_iters")
         shape = dict(kernel=kname, dim=D, chains_per_gpu=N, iters_per_step=S, window_rows=R,
                      stream_diag=bool(a.stream_diag), rho=a.rho)
+        if mass:
+            shape["cov_p_rho"] = a.cov_p_rho
         pm = pmc_traffic(shape)
         # PMC bytes are per hot-kernel DISPATCH (summarize_profile.py averages the timed dispatches);
         # kernel_ms times the step's dispatches together, so the step's traffic is dispatches x that
@@ -546,6 +555,8 @@ def main():
             roof["telemetry"] = telemetry
         tdesc = f"rho={a.rho} dense-precision MVN" if a.rho != 0 else "unit MVN"
         samp = f"NUTS d_max={a.d_max} (overflow counted, not aborted)" if nuts else "Random-L HMC, L~U{5..19}"
+        if mass:
+            samp += f", full cov_p (correlation {a.cov_p_rho})"
         store_desc = (f"every q_chain row, E, dE stored (circular window of {R} rows)" if store else
                       "rows fed to streaming diagnostics" if sd is not None else "no q_chain rows (ablation)")
         line = {

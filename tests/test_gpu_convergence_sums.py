@@ -155,3 +155,29 @@ def test_convergence_stats_mfma_window_vs_oracle(D):
     R_ref, neff_ref = O.convergence_stats(x[:, 1:, :], thin_rate=1, warm_up_num=0)
     np.testing.assert_allclose(R, R_ref, rtol=1e-10)
     np.testing.assert_allclose(neff, neff_ref, rtol=1e-8)
+
+
+@pytest.mark.parametrize("n,slope", [(99, 1e3), (200, 1e3), (128, 1e5)])
+def test_mfma_trending_halves_vs_numpy(n, slope):
+    """Complete passes on the matrix cores (96 <= n <= 208) use V_t = sum sq + sum sq - 2 C_t, an
+    expanded form that cancels when the samples drift far from the series' first sample (advisor
+    r05): strongly trending split halves, x = slope * t + noise.  The sums still equal a float64
+    NumPy restatement of the difference form to the suite's tolerance, and R-hat / ESS equal the
+    oracle's convergence_stats (utils.py:77-179)."""
+    from hmc_amd.diagnostics import _Split, convergence_stats, convergence_sums
+    from oracle import hmc_oracle as O
+    rs = np.random.default_rng(n)
+    N, D = 12, 9
+    rows = 2 * n + 1
+    t = np.arange(rows, dtype=np.float64)
+    q = slope * t[None, :, None] * np.linspace(0.5, 1.5, D)[None, None, :] + rs.normal(size=(N, rows, D))
+    dev = torch.as_tensor(q).cuda()
+    sp = _Split(dev, 1, 1)
+    assert sp.n == n
+    got = convergence_sums(sp, n - 2).cpu().numpy()
+    want = _expected(q[:, 1:], n, n - 2)
+    np.testing.assert_allclose(got, want, rtol=1e-9, atol=1e-12 * np.abs(want).max())
+    R, neff = convergence_stats(dev[:, 1:, :], thin_rate=1, warm_up_num=0)
+    R_ref, neff_ref = O.convergence_stats(q[:, 1:, :], thin_rate=1, warm_up_num=0)
+    np.testing.assert_allclose(R, R_ref, rtol=1e-9)
+    np.testing.assert_allclose(neff, neff_ref, rtol=1e-8)

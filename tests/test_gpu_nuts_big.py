@@ -141,11 +141,12 @@ def test_nuts_large_D_philox_stationary_and_shards():
 
 
 @pytest.mark.parametrize("fp_mode", ["exact", "fast"])
-@pytest.mark.parametrize("D", [136, 330])
+@pytest.mark.parametrize("D", [136, 300, 330])
 def test_nuts_large_D_full_cov_p_vs_oracle(D, fp_mode):
     """A full (non-diagonal) cov_p above D = 128 (samplers.py:352-356, :811-839 through
-    gen_sample_NUTS): the per-chain kernel's GEMVs (kick = inv_cov_p . P x, K = p.inv_cov_p.p,
-    V from P x) on replayed draws vs the oracle; plus Philox determinism."""
+    gen_sample_NUTS): at D = 136 and 300 the lockstep kernel's block GEMMs (round 6: P x, the kick
+    inv_cov_p . P x, and inv_cov_p p for K), at D = 330 the per-chain kernel's GEMVs, on replayed
+    draws vs the oracle; plus Philox determinism."""
     import make_golden_shapes as S
     from hmc_amd import _lib as H
     from hmc_amd.engine import NutsEngine
@@ -237,3 +238,41 @@ def test_nuts_large_D_streaming_and_resume(tmp_path):
     assert torch.equal(b.q, ref.q)
     assert torch.equal(b.q_chain, ref.q_chain)
     np.testing.assert_array_equal(b.read_counters(), ref.read_counters())
+
+
+@pytest.mark.parametrize("D,full", [(200, False), (136, True), (330, True)])
+def test_nuts_large_D_deep_tree_vs_oracle(D, full):
+    """Trees of more than 2^15 points above D = 128 (advisor r05: d_max was raised to 30 on every
+    NUTS kernel, but only the D = 2 tree kernel ran a tree deeper than 15): the lockstep kernel at
+    D = 200 (diagonal cov_p) and D = 136 (full cov_p), the per-chain kernel at D = 330 (full cov_p),
+    d_max = 18, one chain, a step small enough that both ends turn only after 2^15 points.  Leapfrog
+    counts, q_chain and E equal the oracle's on the same replayed draws; no d_max hit."""
+    import make_golden_shapes as S
+    from hmc_amd import _lib as H
+    from hmc_amd.engine import NutsEngine
+    from hmc_amd.target import MVNTarget
+    N, Niter, d_max = 1, 1, 18
+    dt = 5e-5 if not full else 1e-4
+    rs = np.random.RandomState(70 + D)
+    cov = np.eye(D)
+    cov_p = S.dense_cov_p(D) if full else None
+    C = np.linalg.cholesky(cov_p) if full else np.eye(D)
+    q_start = rs.standard_normal((N, D))
+    p0 = rs.standard_normal((N, D)) @ C.T
+    P = rs.standard_normal((N, Niter, D)) @ C.T
+    tape = rs.uniform(0.0, 2.0, (N, Niter * 2 * ((1 << 17) + d_max + 2)))
+    tgt = FastMVN(np.zeros(D), cov)
+    ref = O.gen_sample_nuts(O.HMCCore(tgt, dt, cov_p), q_start, N, Niter, 0, 1, d_max,
+                            O.ReplayDraws(p0, P, tape=tape.copy()), on_dmax="break")
+    assert ref["n_leapfrog"] > 1 << 15, ref["n_leapfrog"]
+    eng = NutsEngine(MVNTarget(np.zeros(D), cov, logdet_const=tgt.c), N, Niter, 0, 1, d_max, dt, cov_p=cov_p,
+                     rng="replay", fp_mode="exact", on_dmax="break")
+    eng.set_replay(p0, P, tape)
+    eng.init(q_start)
+    eng.run(1, Niter + 1)
+    torch.cuda.synchronize()
+    c = eng.read_counters()
+    assert int(c[H.CNT_DMAX]) == 0 and int(c[H.CNT_OOB_REJECT]) == 0
+    assert int(c[H.CNT_LEAPFROG]) == ref["n_leapfrog"]
+    np.testing.assert_allclose(eng.q_chain.cpu().numpy(), ref["q_chain"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(eng.E_chain.cpu().numpy(), ref["E_chain"], rtol=1e-10, atol=1e-10)

@@ -352,9 +352,9 @@ int64_t hmc_random_workspace_size(const hmc_target* t, int64_t n_chains) {
 int64_t hmc_nuts_workspace_size_ex(int32_t D, int64_t n_chains, int32_t d_max, int32_t iters_per_call,
                                    int32_t philox_momenta) {
   if (D < 1 || n_chains < 0 || d_max < 1 || d_max > hmc::kNutsDmaxMax || iters_per_call < 1) return 0;
-  if (hmc::nuts_lock_path(D)) {   // a full cov_p (philox_momenta 0) takes the per-chain kernel at any D > 128
-    const int64_t lock = hmc::nuts_lock_ws_doubles(n_chains, D, d_max);
-    return (philox_momenta ? lock : std::max(lock, hmc::nuts_big_ws_doubles(n_chains, D, d_max))) *
+  if (hmc::nuts_lock_path(D)) {   // philox_momenta 0: replay tapes, or a full cov_p (its fragments too)
+    return (philox_momenta ? hmc::nuts_lock_ws_doubles(n_chains, D, d_max, false)
+                           : hmc::nuts_lock_ws_doubles(n_chains, D, d_max, true)) *
            (int64_t)sizeof(double);
   }
   if (!hmc::dense_tiles(D)) return hmc::nuts_big_ws_doubles(n_chains, D, d_max) * (int64_t)sizeof(double);
@@ -456,7 +456,7 @@ hmc_status hmc_nuts_iters(const hmc_target* t, const hmc_kinetic* k, const hmc_s
   }
   a.traj_q = nullptr;
   a.n_save = 0;
-  if (big && hmc::nuts_lock_path(t->D) && !k->minv_full)   // 128 < D <= 320: lockstep 16-chain blocks
+  if (big && hmc::nuts_lock_path(t->D))   // 128 < D <= 320: lockstep 16-chain blocks (any cov_p)
     return hip_status(hmc::launch_nuts_lock(a, s->fp_mode == HMC_MODE_EXACT, replay, (hipStream_t)stream),
                       "hmc_nuts_iters(lockstep)");
   if (big) return hip_status(hmc::launch_nuts_big(a, s->fp_mode == HMC_MODE_EXACT, replay, (hipStream_t)stream),

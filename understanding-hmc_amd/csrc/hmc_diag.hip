@@ -609,6 +609,10 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
                                                                                              double* partial) {
   // capacity of this instance: NTM tiles, NTM - 1 anchor steps, n <= 16 (NTM - 1)
   constexpr int kNB = NTM - 1, kRows = NTM - 1;
+  // the host takes this instance for 16 (NTM - 3) < n <= 16 (NTM - 1) (launch_conv_mfma): slices
+  // q <= kQAll always hold a row below n, and staging rows 16 i + 15 < n for i < kQAll (NTM = 6, below
+  // the matrix-core range's lower bound, keeps every test)
+  constexpr int kQAll = NTM == 6 ? -1 : NTM - 3;
   // LDS: [4 chains][dims] series of the group at k PK + w P (bank-spread for both the staging writes
   // and the matrix waves' slice reads), x0[16], slack, sq rows [dims][4 chain lanes][272]
   extern __shared__ double lds[];
@@ -621,25 +625,35 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
   const int r = (local / a.G) * 8 + (id & 7), g = local % a.G;
   const Src& s = a.s;
   const int n = s.n, D = s.D, P = a.P, PK = a.PK;
+  // (PAIR: two staged groups per pair of barriers in two LDS buffers, measured 48.1 -> 50.5 ms at
+  // c4's halves; a second staging buffer two groups ahead: 48.1 -> 48.3 ms.  Neither is kept.)
+  constexpr bool PAIR = false;
+  constexpr int NBUF = PAIR ? 2 : 1;
+  constexpr bool SQR_LDS = NTM > 10;               // the sq rows live in LDS (else in registers)
   const int SB = 4 * PK;
-  double* const x0l = lds + SB;
-  double* const sqb = x0l + kMfmaSer + kMfmaSlack;
+  double* const x0l = lds + NBUF * SB;
+  double* const sqb = x0l + NBUF * kMfmaSer + kMfmaSlack;
   const int64_t m2 = n_series(s);
   const int64_t jlo = (int64_t)r * a.per;
   const int64_t jhi = jlo + a.per < m2 ? jlo + a.per : m2;
-  for (int i = tid; i < SB + kMfmaSer + kMfmaSlack + kMfmaSer * kSqStride; i += kMfmaThreads) lds[i] = 0.0;
+  for (int i = tid; i < NBUF * (SB + kMfmaSer) + kMfmaSlack + (SQR_LDS ? kMfmaSer * kSqStride : 0); i += kMfmaThreads)
+    lds[i] = 0.0;
   // staging role: wave = chain sk of the group, lane = (dim sw, row phase rho); rows rho + 16 i
   const int sk = wv, sw = lane & 3, rho = lane >> 2;
   const int sd = g * kMfmaDims + sw;
-  double xs[kRows];
-  double x0s = 0.0;
+  // staged rows of a chain group: two buffers, so that a group's loads are issued two groups
+  // ahead of their LDS stores (one group of matrix work did not cover the HBM latency); the
+  // largest instance (NTM = 14) has no registers left for the second and keeps one group ahead
+  constexpr bool PF2 = PAIR;
+  double xsa[kRows], xsb[PF2 ? kRows : 1];
+  double x0a = 0.0, x0b = 0.0;
   // buffer loads based at the group's first split chain (uniform): one 32-bit lane offset (host-
   // checked below kLagOOB) plus 16 i rows (in the vector offset: the range check covers it); the
   // buffer ends with the view's last sample, so lanes past the range or the dims (offset kLagOOB)
   // and rows past the last chain's end read zeros (y = 0 - 0)
   const int rowb = (int)(s.sample_stride * 8);
   const double* const vend = split_ptr(s, m2 - 1, n - 1) + D;
-  auto stage_load = [&](int64_t jg) {
+  auto stage_load = [&](int64_t jg, double (&xs)[kRows], double& x0s) {
     const int64_t j = jg + sk;
     const double* b = uni(split_ptr(s, jg, 0));
     const int64_t span = (vend - b) * 8;
@@ -651,14 +665,14 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
     for (int i = 0; i < kRows; ++i)
       xs[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lo + 16 * i * rowb, 0, 0));
   };
-  auto stage_store = [&](int nn) {
-    double* dst = lds + sk * PK + sw * P + 16 + rho;
+  auto stage_store = [&](int nn, const double (&xs)[kRows], double x0s, int buf) {
+    double* dst = lds + buf * SB + sk * PK + sw * P + 16 + rho;
 #pragma unroll
     for (int i = 0; i < kRows; ++i) {
-      if (16 * i + 15 < nn) dst[16 * i] = xs[i] - x0s;                    // whole 16-row phase
+      if (i < kQAll || 16 * i + 15 < nn) dst[16 * i] = xs[i] - x0s;      // whole 16-row phase
       else if (16 * i < nn && rho + 16 * i < nn) dst[16 * i] = xs[i] - x0s;   // rows >= n stay zero
     }
-    if (rho == 0) x0l[sk * 4 + sw] = x0s;
+    if (rho == 0) x0l[buf * kMfmaSer + sk * 4 + sw] = x0s;
   };
   // matrix role: wave wv = dimension d; lane = (chain k = lane >> 4, t' or s = lane & 15)
   const int d = g * kMfmaDims + wv;
@@ -679,47 +693,68 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
   const int NT = a.NT;
   const double dn = n;
   const double rn = 1.0 / dn, rn1 = 1.0 / (dn - 1.0);
-  int64_t jg = jlo;
-  if (jg < jhi) stage_load(jg);
-  for (; jg < jhi; jg += 4) {
-    int nn = n;                                   // opaque per group: bounds recomputed, not hoisted
-    asm volatile("" : "+s"(nn));
-#ifndef HMC_MFMA_DEV_NOSTAGE                      // dev timing variant: matrix work on stale LDS
-    __syncthreads();                              // the previous group's slices are read
-    stage_store(nn);
-    __syncthreads();
-    if (jg + 4 < jhi) stage_load(jg + 4);         // in flight under this group's matrix work
-#endif
+  if (jlo < jhi) stage_load(jlo, xsa, x0a);
+  if constexpr (PF2) {
+    if (jlo + 4 < jhi) stage_load(jlo + 4, xsb, x0b);
+  }
+  auto matrix = [&](int64_t jg, int nn, int buf) {
     if (d < D) {
-      int zo = k * PK + wv * P + 16;              // (an opaque integer offset keeps sr an LDS pointer)
+      int zo = buf * SB + k * PK + wv * P + 16;   // (an opaque integer offset keeps sr an LDS pointer)
       asm volatile("" : "+v"(zo));
       const double* sr = lds + zo;
-      // Anchor steps b = 16 bi + 15 (anchors b - 15 .. b: step 0 starts at anchor 0).  Tile ti
-      // (T = 16 (ti - 1)) runs the steps whose anchors still meet a lag >= max(T, 0) below n:
-      // ti <= tl(bi) = v + 1 - bi, v = (n - 1) / 16, bi <= v.  Step-major: a step's tiles are
+      // Anchor steps b = 16 bi + 15 (anchors b - 15 .. b: step 0 starts at anchor 0).  Every
+      // product of tile ti (T = 16 (ti - 1)) at step bi pairs an anchor with row b + T + t' >=
+      // 16 (bi + ti) - 1, so the tile meets a row below n only while 16 (bi + ti) <= n:
+      // ti <= tl(bi) = n / 16 - bi (round 6: the bound was (n - 1) / 16 + 1 - bi, one tile per step
+      // of LDS-zero rows unless 16 | n: 7 of 35 MFMAs per group at n = 99, 13 of 104 at
+      // n = 200).  Steps bi <= v = (n - 1) / 16.  Step-major: a step's tiles are
       // independent accumulators back to back (a tile's own chain of dependent MFMAs ran 20-40 %
       // slower).  Tile ti at step bi reads A slice q = bi + ti (rows 16 (q - 1) + 15 + t'): the
       // slices q = 0 .. NTM are read once, up front, into registers; B of the next step is read a
       // step ahead.  Reads past row n + 29 land in the next series or the LDS slack, feed no MFMA.
-      const int v = (nn - 1) >> 4;
+      const int vt = nn >> 4;                     // tiles ti <= vt - bi meet rows below n
+#ifdef HMC_MFMA_EDGE44
+      const int e4 = ((nn & 15) >> 2) + 1;        // row groups of the edge tiles (4: a whole tile)
+#endif
       double sl[NTM + 1];
 #pragma unroll
       for (int q = 0; q <= NTM; ++q) sl[q] = sr[16 * (q - 1) + 15 + c16];
       double bcur = sr[15 - c16];
       auto bstep = [&](auto bi_c) {
         constexpr int bi = decltype(bi_c)::value;
-        const int tl = min(NT - 1, v + 1 - bi);
+        const int tl = min(NT - 1, vt - bi);
         const double bnx = bi + 1 < kNB ? sr[16 * (bi + 1) + 15 - c16] : 0.0;
         auto tile = [&](auto ti_c) {
           constexpr int ti = decltype(ti_c)::value;
           if constexpr (bi + ti <= NTM) {
+#ifdef HMC_MFMA_EDGE44
+            if (ti < tl || (ti == tl && e4 == 4)) {
+#else
             if (ti <= tl) {
+#endif
 #ifdef HMC_MFMA_DEV_NOLDS                         // dev timing variant: no LDS operands
               acc[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(dn, dn, acc[ti], 0, 0, 0);
 #else
               acc[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(sl[bi + ti], bcur, acc[ti], 0, 0, 0);
 #endif
             }
+#ifdef HMC_MFMA_EDGE44
+            else if (ti == tl) {
+              // the step's edge tile: rows 16 (bi + ti) - 1 + t' < n only for t' <= n % 16, i.e.
+              // accumulator components g < e4 (rows 4 g .. 4 g + 3).  Each takes one
+              // v_mfma_f64_4x4x4f64 (a quarter of the 16x16x4 cost): its four blocks share the A
+              // rows (A lane (k, blk, i) = y_k[row 4 g + i]), B is the 16x16x4 operand as it is
+              // (lane (k, s)), and its result lane (i, blk, j) is entry (4 g + i, 4 blk + j) --
+              // the lane and component g where the 16x16x4 layout keeps that entry.
+#pragma unroll
+              for (int g = 0; g < 3; ++g) {
+                if (g < e4) {
+                  const double a4 = sr[16 * (bi + ti - 1) + 15 + 4 * g + (c16 & 3)];
+                  acc[ti][g] = __builtin_amdgcn_mfma_f64_4x4x4f64(a4, bcur, acc[ti][g], 0, 0, 0);
+                }
+              }
+            }
+#endif
           }
         };
         static_for<NTM>(tile);
@@ -736,13 +771,15 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
       const int qn = nn >> 4;                     // slices past q = n / 16 hold rows >= n only
 #pragma unroll
       for (int q = 0; q <= kRows; ++q) {
-        if (q <= qn) {                            // (rows n .. n + 29 of slice qn are LDS zeros)
-          const double y = sl[q];
-          ps1 += y;
-          ps2 = __builtin_fma(y, y, ps2);
-          if constexpr (SQR) sqr[q] = __builtin_fma(y, y, sqr[q]);
-          else sqa[16 * q + c16] = __builtin_fma(y, y, sv[q]);   // sq row 16 q + t' - 1
-        }
+        // (rows n .. n + 29 of slice qn are LDS zeros; later slices may read the next series).
+        // Only the last slices of an instance can lie past qn (kQAll): one select there, instead of
+        // a guarded update per slice that the compiler turned into six v_cndmask per slice
+        double y = sl[q];
+        if (q > kQAll) y = q <= qn ? y : 0.0;
+        ps1 += y;
+        ps2 = __builtin_fma(y, y, ps2);
+        if constexpr (SQR) sqr[q] = __builtin_fma(y, y, sqr[q]);
+        else if (q <= kQAll || q <= qn) sqa[16 * q + c16] = __builtin_fma(y, y, sv[q]);   // sq row 16 q + t' - 1
       }
 #pragma unroll
       for (int m = 1; m < 16; m <<= 1) {
@@ -752,10 +789,31 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
       if (jg + k < jhi) {
         const double mm2 = ps2 - ps1 * (ps1 * rn);
         a_std += sqrt(mm2 > 0.0 ? mm2 * rn1 : 0.0);
-        const double e = (x0l[k * 4 + wv] - Sd) + ps1 * rn;
+        const double e = (x0l[buf * kMfmaSer + k * 4 + wv] - Sd) + ps1 * rn;
         a_m += e;
         a_m2 = __builtin_fma(e, e, a_m2);
       }
+    }
+  };
+  for (int64_t jg = jlo; jg < jhi; jg += 4 * NBUF) {
+    int nn = n;                                   // opaque per group: bounds recomputed, not hoisted
+    asm volatile("" : "+s"(nn));
+#ifndef HMC_MFMA_DEV_NOSTAGE                      // dev timing variant: matrix work on stale LDS
+    __syncthreads();                              // the previous groups' slices are read
+    stage_store(nn, xsa, x0a, 0);
+    if constexpr (PAIR) {
+      if (jg + 4 < jhi) stage_store(nn, xsb, x0b, 1);
+    }
+    __syncthreads();
+    // the next groups' rows in flight under this pair's matrix work
+    if (jg + 4 * NBUF < jhi) stage_load(jg + 4 * NBUF, xsa, x0a);
+    if constexpr (PAIR) {
+      if (jg + 12 < jhi) stage_load(jg + 12, xsb, x0b);
+    }
+#endif
+    matrix(jg, nn, 0);
+    if constexpr (PAIR) {
+      if (jg + 4 < jhi) matrix(jg + 4, nn, 1);
     }
   }
   // partial of this wave: tiles (entry t' * 16 + s), sq rows (summed over the 4 chain lanes; LDS
@@ -1207,7 +1265,9 @@ bool mfma_ok(const Src& s, int T) {
 
 // the samples, x0, the slack for the read-ahead past the last series, the sq rows
 size_t mfma_lds(const MfmaArgs& a) {
-  return (size_t)(4 * a.PK + kMfmaSer + kMfmaSlack + kMfmaSer * kSqStride) * sizeof(double);
+  // k_conv_mfma<NTM <= 10> (n <= 144) keeps the sq rows in registers: no LDS for them
+  const bool small = a.s.n <= 16 * 9;
+  return (size_t)(4 * a.PK + kMfmaSer + kMfmaSlack + (small ? 0 : kMfmaSer * kSqStride)) * sizeof(double);
 }
 
 int64_t mfma_work(const MfmaArgs& a) {

@@ -50,7 +50,7 @@ struct RandArgs {
   int n_save, traj_stride;
   int Lq, q_row0;        // q_chain buffer: rows per chain (row r at r % Lq) and the first row stored
   int d_max, on_dmax;    // NUTS (hmc_nuts.hip)
-  unsigned wait_cap;     // NUTS: wave steps a slot waits for a chain hand-off before giving up
+  uint64_t wait_cap;     // NUTS: wave steps a slot waits for a chain hand-off before giving up
   int nuts_kb;           // NUTS: iterations of the launch's chain-affine block units (0: tree units only)
   double* ws;            // NUTS per-chain workspace (vectors: live points, boundaries, save slots)
   const double* tape;    // NUTS replay tape [n][tape_stride] (directions / uniforms in consumption order)
@@ -79,7 +79,7 @@ int64_t nuts_big_ws_doubles(int64_t n, int D, int d_max);
 // NUTS for 128 < D <= 320 in lockstep 16-chain blocks (hmc_nuts_lock.hip): one MFMA GEMM per block
 // step gives every chain its gradient
 bool nuts_lock_path(int D);
-int64_t nuts_lock_ws_doubles(int64_t n, int D, int d_max);
+int64_t nuts_lock_ws_doubles(int64_t n, int D, int d_max, bool mass);
 hipError_t launch_nuts_lock(const RandArgs& a, bool exact, bool replay, hipStream_t s);
 hipError_t launch_nuts_big(const RandArgs& a, bool exact, bool replay, hipStream_t s);
 

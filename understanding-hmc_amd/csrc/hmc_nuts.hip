@@ -58,13 +58,15 @@ enum : int { S_ITER_START = 0, S_READY = 2, S_ITER_END = 3, S_DONE = 4, S_FETCH 
              S_WAIT = 8 };
 
 // Chain hand-off between slots (any CU, any XCD) inside a launch: the chain's state (q, E_prev, tape
-// cursor) is stored write-through (relaxed agent-scope atomic stores, sc1) and drained
-// (vmcnt(0)) before one lane publishes the chain's iteration count with a relaxed agent-scope
-// store; the taking slot polls that word and reads the state with sc1 loads, which bypass its
-// CU's L1 (cdna_hip_programming.md Guideline 16, R1).  The HIP memory model's agent-scope release
-// store / acquire load would add an L2 writeback (buffer_wbl2 sc1) per publish and an L2
-// invalidate (buffer_inv sc1) per poll; measured on the c5 launch (scripts/dev/ab_libs.sh,
-// HMC_NUTS_RELACQ build): 1.761e9 -> 1.667e9 lf/s (-5%), so the sc1 + vmcnt protocol stays.
+// cursor) is stored with relaxed agent-scope atomic stores (write-through, sc1) and drained
+// (vmcnt(0)); then, following the HIP memory model, one agent-scope RELEASE fence per wave step
+// that publishes orders those stores before the relaxed store of the chain's iteration count; the
+// taking slot polls that word with relaxed loads and, in the step a poll succeeds, issues one
+// agent-scope ACQUIRE fence before its (sc1) state loads: fence-fence synchronisation, so the
+// hand-off holds on any memory system the model covers, not only on today's gfx950 caches.  With
+// chain affinity (hand-offs once per kNutsBlock trees) it costs 2.5% against the relaxed sc1 +
+// vmcnt protocol alone (1.934e9 vs 1.982e9 lf/s, same box; -5 to -6% with a hand-off per tree);
+// that protocol stays as the dev A/B variant HMC_NUTS_RELAXED.
 // Reserving the next unit at tree start and polling its chain during the tree (so that a tree's
 // end costs one round trip) measured 1.77e9 -> 1.52e9 lf/s: those loads sit in the in-order vmcnt
 // queue ahead of the U-turn checks' loads, which then wait for them.
@@ -89,12 +91,13 @@ __device__ __forceinline__ double ld_wt_d(const double* p) {
 // the factor 4 covers the difference.  A holder can still be slowed far more than that (clock or
 // XCD variation, several ranks sharing one GPU), so the cap never drops below 2^20 wave steps: a
 // give-up is a hard error and only a broken hand-off may trip it.
-inline unsigned nuts_wait_cap(int64_t slots, int64_t n, int d_max, int kb) {
+// 64-bit counter and cap (advisor r05): at d_max >= 27 a block of 8 legitimate deep trees exceeds
+// 2^31 wave steps, and a 32-bit clamp would turn a slow but healthy hand-off into a give-up.
+inline uint64_t nuts_wait_cap(int64_t slots, int64_t n, int d_max, int kb) {
   const int64_t inflight = (slots + n - 1) / std::max<int64_t>(n, 1) + 1;
   // a block unit holds its chain for kb trees (wait: the chain's previous unit)
   const int64_t trees = std::max(kb, 1);
-  const int64_t cap = std::max<int64_t>(4 * inflight * trees * ((int64_t(1) << (d_max + 1)) + 64), int64_t(1) << 20);
-  return (unsigned)std::min<int64_t>(cap, 0x7FFFFFFF);
+  return (uint64_t)std::max<int64_t>(4 * inflight * trees * ((int64_t(1) << (d_max + 1)) + 64), int64_t(1) << 20);
 }
 
 // workspace vector ids (per chain).  The live points old/new (:577, :623, :750, :775) are two
@@ -360,7 +363,7 @@ void k_nuts_iters(RandArgs a) {
   const int n_blk = (a.nuts_kb + kNutsBlock - 1) / kNutsBlock;   // block units per chain
   const unsigned long long nb = (unsigned long long)a.n * (unsigned long long)n_blk;
   const unsigned long long n_units = nb + (unsigned long long)a.n * (unsigned long long)(a.it1 - a.it0 - a.nuts_kb);
-  unsigned waited = 0;
+  uint64_t waited = 0;
   int it_last = 0;                                      // the current unit's last iteration
   int64_t c = 0;
   bool live = false;
@@ -450,9 +453,9 @@ void k_nuts_iters(RandArgs a) {
       }
       if (__builtin_amdgcn_ballot_w64(state == S_FETCH && live)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the state has reached L2/memory ...
-#ifdef HMC_NUTS_RELACQ
-        // A/B variant on the HIP memory model: one agent-scope release fence per wave step that
-        // publishes (an L2 write-back across XCDs), then relaxed atomic publishes
+#ifndef HMC_NUTS_RELAXED
+        // one agent-scope release fence per wave step that publishes (an L2 write-back across
+        // XCDs), then relaxed atomic publishes
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         if (state == S_FETCH && live && h == 0)
           __hip_atomic_store(done + c, (unsigned)(it + 1 - a.it0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -495,8 +498,8 @@ void k_nuts_iters(RandArgs a) {
         const unsigned need = (unsigned)(it - a.it0);
         bool ready = need == 0;
         if (!ready) {
-#ifdef HMC_NUTS_RELACQ
-          // relaxed polls; the acquire fence (an L2 invalidate) once, in the step a poll succeeds
+#ifndef HMC_NUTS_RELAXED
+          // relaxed polls; the acquire fence (an L1 invalidate) once, in the step a poll succeeds
           ready = __hip_atomic_load(done + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need;
           if (__builtin_amdgcn_ballot_w64(ready)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #else

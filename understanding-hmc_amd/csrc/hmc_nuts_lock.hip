@@ -17,6 +17,11 @@
 //      finishes the step: second half kick, energy, the new point's bookkeeping (saves at slot
 //      ctz(l - 1), U-turn checks against check_points, progressive sampling), the sub-tree end
 //      (biased acceptance, termination).
+// A full cov_p (MASS, samplers.py:352-356, :811-839; round 6) adds block GEMMs on the same fragment
+// machinery, as the reference writes the products: the kick kv = inv_cov_p (P x) (a second GEMM on
+// the 16 gradients), K = p.inv_cov_p.p (a GEMM on the 16 momenta after the second half kick) and,
+// when a chain of the block starts an iteration in Philox mode, p = C z (C = chol(cov_p)); the tree
+// ends then keep kv in their g slot (a doubling restarted from an end kicks with it).
 // Chains come from a launch-wide queue; a slot runs all of a chain's iterations of the launch, then
 // writes the chain back and takes the next one, so no chain changes slots inside a launch.
 // Draws are the ones hmc_nuts_big.hip makes (replay tape / Philox keyed (slot, iteration, chain)),
@@ -47,6 +52,8 @@ enum : int { LS_FETCH = 0, LS_GRAD = 1, LS_LEAP = 2, LS_DONE = 3 };
 struct LockGeom {
   int NT, KS, F;                  // output tiles (16 rows), k-steps (4), fragments NT * KS
   const double* pf;               // precision fragments [F][64]
+  const double* mf;               // MASS: inv_cov_p fragments [F][64]
+  const double* cf;               // MASS, Philox: chol(cov_p) fragments [F][64]
   double* slots;                  // per slot: lock_nvec vectors of 64 * kLockJ doubles
   unsigned long long* queue;      // next chain of the launch (zeroed per launch)
   int64_t* tcur;                  // per chain replay-tape cursor (persists across launches)
@@ -54,14 +61,15 @@ struct LockGeom {
 
 // fragment f = nt * KS + ks of the precision, lane l: P[16 nt + (l & 15)][4 ks + (l >> 4)] (zero
 // padded): the A operand of v_mfma_f64_16x16x4f64, one coalesced 512-B row per fragment
+// (trans: the matrix is passed transposed, as hmc_kinetic.p_chol_t = C^T)
 __global__ __launch_bounds__(256) void k_lock_pfrag(const double* __restrict__ prec, int D, int KS, int64_t F,
-                                                    double* __restrict__ pf) {
+                                                    double* __restrict__ pf, int trans) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < F * 64; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t f = i >> 6;
     const int l = (int)(i & 63);
     const int nt = (int)(f / KS), ks = (int)(f - (int64_t)nt * KS);
     const int row = 16 * nt + (l & 15), col = 4 * ks + (l >> 4);
-    pf[i] = (row < D && col < D) ? prec[(int64_t)row * D + col] : 0.0;
+    pf[i] = (row < D && col < D) ? prec[trans ? (int64_t)col * D + row : (int64_t)row * D + col] : 0.0;
   }
 }
 
@@ -73,12 +81,13 @@ __device__ __forceinline__ int save_slot_l(int l, int d_max) { return l == 1 ? d
 
 // J: coordinates per lane (D <= 64 J): instances J = 3 (D <= 192) and kLockJ, so that the
 // per-chain work of a smaller D issues no fully masked slots (and holds fewer registers)
-template <bool EXACT, bool REPLAY, int J>
+template <bool EXACT, bool REPLAY, int J, bool MASS>
 __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom G) {
   __shared__ double sX[kLockDmax * kLockXS];                 // x of the 16 chains, [k][chain]
   __shared__ double sSeg[kLockSegMax * 16 * kLockXS];        // partial output tiles, [row][chain]
   __shared__ double tab[REPLAY ? 2 : kNormalTableDoubles];   // Box-Muller tables (Philox momenta)
   __shared__ int sAlive[kLockW];
+  __shared__ int sGrad[kLockW];                              // MASS: slots at an iteration start
   if constexpr (!REPLAY) init_normal_tables(tab);
   const int lane = threadIdx.x & (kWave - 1);
   const int w = uniform_i(threadIdx.x / kWave);
@@ -93,6 +102,10 @@ __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom 
   const int lo8 = lane * 8;
   const __amdgpu_buffer_rsrc_t rpf = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(G.pf), 0, G.F * 512,
                                                                       0x00020000);
+  const __amdgpu_buffer_rsrc_t rmf = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(MASS ? G.mf : G.pf), 0,
+                                                                      G.F * 512, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rcf = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>((MASS && G.cf) ? G.cf : G.pf),
+                                                                      0, G.F * 512, 0x00020000);
   auto wget = [&](int id, int j) -> double {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rws, lo8 + 512 * j, id * Dp * 8, 0));
   };
@@ -144,9 +157,12 @@ __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom 
   auto dps = [&](int j) { return a.pscale ? dget(rps, j) : 1.0; };
   auto wsum = [&](double s) { return wave_sum_dpp(s); };
 
-  double q[J], p[J], g[J];
+  // g = P x; MASS: kv = inv_cov_p g (the kick), and the tree ends keep kv in their g slot
+  double q[J], p[J], g[J], kv[MASS ? J : 1], u[MASS ? J : 1];
 #pragma unroll
   for (int j = 0; j < J; ++j) q[j] = p[j] = g[j] = 0.0;
+#pragma unroll
+  for (int j = 0; j < (MASS ? J : 1); ++j) kv[j] = u[j] = 0.0;
   int state = LS_FETCH;
   int64_t c = 0;
   uint64_t gc = 0;
@@ -193,10 +209,16 @@ __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom 
       const int dd = lane + 64 * j;
       if (dd < D) {
         maha += (q[j] - dq0(j)) * g[j];
-        kin += p[j] * (dminv(j) * p[j]);
+        if constexpr (MASS) kin += p[j] * u[j];                 // p . (inv_cov_p p)
+        else kin += p[j] * (dminv(j) * p[j]);
       }
     }
     return 0.5 * (a.logc + (wsum(maha) + wsum(kin)));
+  };
+  // the "g" slot of a tree end: the kick vector (MASS) or the gradient
+  auto gslot = [&]() -> double (&)[J] {
+    if constexpr (MASS) return kv;
+    else return g;
   };
 
   while (true) {
@@ -227,31 +249,43 @@ __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom 
       for (int j = 0; j < J; ++j) {
         const int dd = lane + 64 * j;
         if (dd < D) {
-          const double dt = ddt(j), mi = dminv(j);
-          p[j] = EXACT ? p[j] - (dt * (mi * g[j])) * 0.5 : __builtin_fma(-0.5 * dt * mi, g[j], p[j]);
+          const double dt = ddt(j);
+          if constexpr (MASS) {                               // kick by inv_cov_p dVdq (Q3)
+            p[j] = EXACT ? p[j] - (dt * kv[j]) * 0.5 : __builtin_fma(-0.5 * dt, kv[j], p[j]);
+          } else {
+            const double mi = dminv(j);
+            p[j] = EXACT ? p[j] - (dt * (mi * g[j])) * 0.5 : __builtin_fma(-0.5 * dt * mi, g[j], p[j]);
+          }
           q[j] = EXACT ? q[j] + dt * p[j] : __builtin_fma(dt, p[j], q[j]);
         }
       }
     }
-    if (state == LS_LEAP || state == LS_GRAD) {
+    const bool busy = state == LS_LEAP || state == LS_GRAD;
+    if (busy) {
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         const int dd = lane + 64 * j;
         if (dd < 4 * KS) sX[dd * kLockXS + w] = dd < D ? q[j] - dq0(j) : 0.0;
       }
     }
-    if (lane == 0) sAlive[w] = state != LS_DONE;
+    if (lane == 0) {
+      sAlive[w] = state != LS_DONE;
+      if constexpr (MASS) sGrad[w] = state == LS_GRAD;
+    }
     __syncthreads();
-    int alive = 0;
+    int alive = 0, any_grad = 0;
 #pragma unroll
-    for (int v = 0; v < kLockW; ++v) alive |= sAlive[v];
+    for (int v = 0; v < kLockW; ++v) {
+      alive |= sAlive[v];
+      if constexpr (MASS) any_grad |= sGrad[v];
+    }
     if (!alive) break;                                      // (uniform over the block)
     if (w == 0) ++n_steps;
 
-    // ================= the block's GEMM: fragments [f0, f1) of G = P X, partial tiles to LDS.
-    // Scalar k-step counter and a running LDS address (no division per MFMA); A fragments through a
-    // buffer descriptor with the fragment's offset in the scalar offset.
-    {
+    // ================= the block's GEMM: fragments [f0, f1) of M X (M = P, or with MASS inv_cov_p /
+    // C), partial tiles to LDS.  Scalar k-step counter and a running LDS address (no division per
+    // MFMA); A fragments through a buffer descriptor with the fragment's offset in the scalar offset.
+    auto gemm = [&](const __amdgpu_buffer_rsrc_t& rm) {
       typedef double d4 __attribute__((ext_vector_type(4)));
       d4 acc = {0.0, 0.0, 0.0, 0.0};
       const int ch = lane & 15, kh = lane >> 4;
@@ -265,7 +299,7 @@ __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom 
         for (int v = 0; v < 4; ++v) t[(4 * v + kh) * kLockXS + ch] = acc[v];
       };
       auto frag = [&](int f) {
-        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rpf, lo8 + f * 512, 0, 0));
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rm, lo8 + f * 512, 0, 0));
       };
       // four fragments in flight in a static register ring (unrolled by four). Every load is issued
       // on every path (past f1: a fragment the wave does not use, or zeros past the buffer), and the
@@ -304,22 +338,75 @@ __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom 
         }
       }
       if (ks != 0) flush();                                 // a tile the range ends inside
-    }
-    __syncthreads();
-    if (state == LS_LEAP || state == LS_GRAD) {             // this chain's gradient rows, segments in order
+    };
+    // this chain's rows of the product, segments in order
+    auto gather = [&](double (&y)[J]) {
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         const int dd = lane + 64 * j;
-        double s = 0.0;
-        for (int t = 0; t < gcnt[j]; ++t) s += sSeg[(gseg[j] + t) * (16 * kLockXS) + (dd & 15) * kLockXS + w];
-        g[j] = s;
+        double sacc = 0.0;
+        for (int t = 0; t < gcnt[j]; ++t) sacc += sSeg[(gseg[j] + t) * (16 * kLockXS) + (dd & 15) * kLockXS + w];
+        y[j] = sacc;
       }
+    };
+    // one more block product: this wave's column x (zero past D) into the tile, the GEMM, its rows
+    auto product = [&](const __amdgpu_buffer_rsrc_t& rm, const double (&x)[J], double (&y)[J], bool put, bool get) {
+      if (put) {
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+          const int dd = lane + 64 * j;
+          if (dd < 4 * KS) sX[dd * kLockXS + w] = dd < D ? x[j] : 0.0;
+        }
+      }
+      __syncthreads();                                      // columns written, the last gather done
+      gemm(rm);
+      __syncthreads();
+      if (get) gather(y);
+    };
+    gemm(rpf);
+    __syncthreads();
+    if (busy) gather(g);                                    // g = P (q - q0)
+    if constexpr (MASS) {
+      product(rmf, g, kv, busy, busy);                      // the kick inv_cov_p dVdq (:835-837)
+      if (state == LS_GRAD) {                               // iteration start: p ~ N(0, cov_p) (:565, :829)
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+          const int dd = lane + 64 * j;
+          double pd = 0.0;
+          if (dd < D) {
+            if constexpr (REPLAY) {
+              pd = a.rp[(c * (int64_t)a.niter + (it - 1)) * D + dd];
+            } else {                                      // z, then p = C z below
+              const int h = dd & 3, jj = dd >> 3;
+              double z0, z1;
+              normal_pair_tab(draw_block((uint32_t)(8 * jj + h), (uint32_t)it, gc, a.k0, a.k1), tab, z0, z1);
+              pd = (dd >> 2) & 1 ? z1 : z0;
+            }
+          }
+          p[j] = pd;
+        }
+      }
+      if constexpr (!REPLAY) {
+        if (any_grad) product(rcf, p, p, state == LS_GRAD, state == LS_GRAD);   // p = C z
+      }
+      if (state == LS_LEAP) {                               // second half kick (:837-839)
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+          const int dd = lane + 64 * j;
+          if (dd < D) {
+            const double dt = ddt(j);
+            p[j] = EXACT ? p[j] - (dt * kv[j]) * 0.5 : __builtin_fma(-0.5 * dt, kv[j], p[j]);
+          }
+        }
+      }
+      product(rmf, p, u, busy, busy);                       // inv_cov_p p for K (:823)
     }
 
     // ================= post-gradient
     if (state == LS_GRAD) {                                 // iteration start (:563-584)
 #pragma unroll
       for (int j = 0; j < J; ++j) {
+        if constexpr (MASS) break;                          // p drawn above (C z / the replay draw)
         const int dd = lane + 64 * j;
         double pd = 0.0;
         if (dd < D) {
@@ -345,10 +432,10 @@ __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom 
       for (int j = 0; j < J; ++j) mp[j] = -p[j];
       vstore(LV_RIGHT, q);                                  // right = (q, p, g), left = (q, -p, g)
       vstore(LV_RIGHT + 1, p);
-      vstore(LV_RIGHT + 2, g);
+      vstore(LV_RIGHT + 2, gslot());
       vstore(LV_LEFT, q);
       vstore(LV_LEFT + 1, mp);
-      vstore(LV_LEFT + 2, g);
+      vstore(LV_LEFT + 2, gslot());
       lo = LV_LIVE;
       vstore(lo, q);                                        // live_point_q_old (:577)
       E_max_old = E_init;
@@ -366,13 +453,14 @@ __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom 
       continue;
     }
     if (state != LS_LEAP) continue;
-    // second half kick (:837-839)
+    if constexpr (!MASS) {                                  // second half kick (:837-839; MASS: above)
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const int dd = lane + 64 * j;
-      if (dd < D) {
-        const double dt = ddt(j), mi = dminv(j);
-        p[j] = EXACT ? p[j] - (dt * (mi * g[j])) * 0.5 : __builtin_fma(-0.5 * dt * mi, g[j], p[j]);
+      for (int j = 0; j < J; ++j) {
+        const int dd = lane + 64 * j;
+        if (dd < D) {
+          const double dt = ddt(j), mi = dminv(j);
+          p[j] = EXACT ? p[j] - (dt * (mi * g[j])) * 0.5 : __builtin_fma(-0.5 * dt * mi, g[j], p[j]);
+        }
       }
     }
     ++n_lf;
@@ -441,7 +529,7 @@ __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom 
       vload(o + 1, op);
       vstore(b, q);
       vstore(b + 1, p);
-      vstore(b + 2, g);
+      vstore(b + 2, gslot());
       const double r_ = exp(-(E_max_now - E_max_old)) * pi_old / pi_new;   // :766 (Q11)
       const double E_max_old_prev = E_max_old;
       E_max_old = fmax(E_max_old_prev, E_max_now);
@@ -471,7 +559,7 @@ __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom 
             q[j] = oq[j];
             p[j] = op[j];
           }
-          vload(o + 2, g);
+          vload(o + 2, gslot());
           udir = nd;
         }
         k = 0;
@@ -528,11 +616,12 @@ int64_t lock_blocks(int64_t n) {
 bool nuts_lock_path(int D) { return D > 128 && D <= kLockDmax; }
 
 // workspace: slot vectors (blocks x 16 slots), precision fragments, queue word, tape cursors
-int64_t nuts_lock_ws_doubles(int64_t n, int D, int d_max) {
+// (mass: the inv_cov_p and chol(cov_p) fragments too)
+int64_t nuts_lock_ws_doubles(int64_t n, int D, int d_max, bool mass) {
   const int NT = (D + 15) / 16, KS = (D + 3) / 4;
   const int64_t blocks = (n + kLockW - 1) / kLockW < 1024 ? (n + kLockW - 1) / kLockW : 1024;
   return (blocks < 1 ? 1 : blocks) * kLockW * (int64_t)lock_nvec(d_max) * 64 * kLockJ +
-         (int64_t)NT * KS * 64 + 2 + n;
+         (int64_t)NT * KS * 64 * (mass ? 3 : 1) + 2 + n;
 }
 
 hipError_t launch_nuts_lock(const RandArgs& a, bool exact, bool replay, hipStream_t s) {
@@ -547,27 +636,41 @@ hipError_t launch_nuts_lock(const RandArgs& a, bool exact, bool replay, hipStrea
   g.slots = a.ws;
   double* pf = a.ws + slot_doubles;
   g.pf = pf;
-  g.queue = reinterpret_cast<unsigned long long*>(pf + (int64_t)g.F * 64);
-  g.tcur = reinterpret_cast<int64_t*>(pf + (int64_t)g.F * 64 + 2);
+  const bool mass = a.minvf != nullptr;
+  double* const after = pf + (int64_t)g.F * 64 * (mass ? 3 : 1);
+  g.mf = mass ? pf + (int64_t)g.F * 64 : nullptr;
+  g.cf = (mass && !replay) ? pf + 2 * (int64_t)g.F * 64 : nullptr;
+  g.queue = reinterpret_cast<unsigned long long*>(after);
+  g.tcur = reinterpret_cast<int64_t*>(after + 2);
   // the partial tiles of one block step: NT plus one per wave boundary inside a tile
   if (g.NT + kLockW - 1 > kLockSegMax || a.D > kLockDmax) return hipErrorInvalidValue;
   if (hipError_t e = hipMemsetAsync(g.queue, 0, sizeof(unsigned long long), s)) return e;
-  k_lock_pfrag<<<(unsigned)std::min<int64_t>(((int64_t)g.F * 64 + 255) / 256, 4096), 256, 0, s>>>(a.prec, a.D, g.KS, g.F,
-                                                                                                  pf);
+  const unsigned fgrid = (unsigned)std::min<int64_t>(((int64_t)g.F * 64 + 255) / 256, 4096);
+  k_lock_pfrag<<<fgrid, 256, 0, s>>>(a.prec, a.D, g.KS, g.F, pf, 0);
+  if (mass) {
+    k_lock_pfrag<<<fgrid, 256, 0, s>>>(a.minvf, a.D, g.KS, g.F, const_cast<double*>(g.mf), 0);
+    if (!replay) k_lock_pfrag<<<fgrid, 256, 0, s>>>(a.cholt, a.D, g.KS, g.F, const_cast<double*>(g.cf), 1);
+  }
   if (hipError_t e = hipGetLastError()) return e;
   const dim3 grid((unsigned)blocks);
-  auto go = [&](auto jc) {
+  auto go = [&](auto jc, auto mc) {
     constexpr int J = decltype(jc)::value;
+    constexpr bool M = decltype(mc)::value;
     if (exact) {
-      if (replay) k_nuts_lock<true, true, J><<<grid, 64 * kLockW, 0, s>>>(a, g);
-      else k_nuts_lock<true, false, J><<<grid, 64 * kLockW, 0, s>>>(a, g);
+      if (replay) k_nuts_lock<true, true, J, M><<<grid, 64 * kLockW, 0, s>>>(a, g);
+      else k_nuts_lock<true, false, J, M><<<grid, 64 * kLockW, 0, s>>>(a, g);
     } else {
-      if (replay) k_nuts_lock<false, true, J><<<grid, 64 * kLockW, 0, s>>>(a, g);
-      else k_nuts_lock<false, false, J><<<grid, 64 * kLockW, 0, s>>>(a, g);
+      if (replay) k_nuts_lock<false, true, J, M><<<grid, 64 * kLockW, 0, s>>>(a, g);
+      else k_nuts_lock<false, false, J, M><<<grid, 64 * kLockW, 0, s>>>(a, g);
     }
   };
-  if (a.D <= 64 * 3) go(std::integral_constant<int, 3>{});
-  else go(std::integral_constant<int, kLockJ>{});
+  if (mass) {
+    if (a.D <= 64 * 3) go(std::integral_constant<int, 3>{}, std::true_type{});
+    else go(std::integral_constant<int, kLockJ>{}, std::true_type{});
+  } else {
+    if (a.D <= 64 * 3) go(std::integral_constant<int, 3>{}, std::false_type{});
+    else go(std::integral_constant<int, kLockJ>{}, std::false_type{});
+  }
   return hipGetLastError();
 }
 

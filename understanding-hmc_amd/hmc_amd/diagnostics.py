@@ -429,6 +429,7 @@ class StreamingDiagnostics:
         self.pos = 0                                                    # samples consumed
         self.mode = mode                                                # "exact" | "stream"; None: the feeder picks
         self.window_rows = None                                         # rows of the feeder's window (first call)
+        self.exact_max_samples = None                                   # feeder: largest n_samples fed exactly
         self._stream_state = None
         self.halves = []                                                # exact: halves added, in order
         self.xsums = None                                               # exact: sums about xshift
@@ -532,13 +533,15 @@ class StreamingDiagnostics:
             T = self.exact_lags()
             R, n_eff, need, Vt, _, _ = rhat_ess_from_sums(self.xsums, self.xshift, 2 * self.N, self.n, T, group)
             assert not need.any()
-            info = dict(mode="streaming-exact", lags=int(Vt.shape[0]), truncated_dims=0, n_half=int(self.n))
+            info = dict(mode="streaming-exact", lags=int(Vt.shape[0]), truncated_dims=0, n_half=int(self.n),
+                        n_samples=2 * int(self.n), exact_max_samples=self.exact_max_samples)
             self.info = info
             LAST_INFO.clear()
             LAST_INFO.update(info)
             return R, n_eff
         mean, std = self.moments()
-        info = dict(mode="streaming", tmax=self.tmax)
+        info = dict(mode="streaming", tmax=self.tmax, n_half=int(self.n), n_samples=2 * int(self.n),
+                    exact_max_samples=self.exact_max_samples)
         out = combine_split_stats(mean, std, self.vsum, self.n, group, info=info)
         self.info = info
         LAST_INFO.clear()

@@ -184,6 +184,8 @@ class RandomEngine:
         # variogram carry) would be silently replaced by a zeroed window (advisor r05)
         if diag.mode is None:
             diag._set_mode("exact" if exact else "stream")
+            # the envelope of the exact mode for this feed: halves of n <= tmax + feed/thin samples
+            diag.exact_max_samples = 2 * (T + feed // self.thin) + 1
         if diag.window_rows is not None and diag.window_rows != W:
             raise AssertionError("run_streaming continued with step/feed giving a %d-row window; the "
                                  "statistics' window has %d rows (use the same step and feed)" % (W, diag.window_rows))
@@ -260,6 +262,7 @@ class RandomEngine:
         meta = dict(self._meta(), it_next=int(it_next), diag_pos=None if diag is None else diag.pos,
                     diag_mode=None if diag is None else diag.mode,
                     diag_window_rows=None if diag is None else diag.window_rows,
+                    diag_exact_max_samples=None if diag is None else diag.exact_max_samples,
                     diag_halves=None if diag is None else list(diag.halves))
         np.savez(path, meta=np.array(json.dumps(meta)), **{k: v.cpu().numpy() for k, v in arr.items()})
 
@@ -282,6 +285,7 @@ class RandomEngine:
             if diag is not None:
                 diag.mode = meta.get("diag_mode")
                 diag.window_rows = meta.get("diag_window_rows")
+                diag.exact_max_samples = meta.get("diag_exact_max_samples")
                 diag.halves = list(meta.get("diag_halves") or [])
                 if diag.mode == "exact":
                     if "diag_xsums" in z.files:

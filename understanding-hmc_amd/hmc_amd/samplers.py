@@ -277,9 +277,11 @@ class HMC_sampler(sampler):
             self.stream_info = dict(diag.info)
             if diag.info["truncated_dims"]:
                 warnings.warn("streaming ESS: %d of %d dimensions need variogram lags beyond stream_tmax=%d; "
-                              "their n_eff is the sum truncated there, not the reference's value "
-                              "(raise stream_tmax or store q_chain)"
-                              % (diag.info["truncated_dims"], self.D, diag.tmax), UserWarning, stacklevel=2)
+                              "their n_eff is the sum truncated there, not the reference's value.  The exact "
+                              "estimator streams up to %s samples per chain (2*(stream_tmax + stream_feed/thin) "
+                              "+ 1); this run has %d: raise stream_feed or store q_chain"
+                              % (diag.info["truncated_dims"], self.D, diag.tmax, diag.info.get("exact_max_samples"),
+                                 diag.info.get("n_samples", 0)), UserWarning, stacklevel=2)
             return
         sampler.compute_convergence_stats(self)
 
