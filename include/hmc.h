@@ -196,7 +196,8 @@ int64_t hmc_random_workspace_size_ex(const hmc_target* t, const hmc_kinetic* k, 
  * Philox runs with a diagonal cov_p (philox_momenta != 0), the momenta drawn ahead of the tree
  * kernel: n_chains x min(32, iters_per_call) x 16*ceil(D/16) doubles (iters_per_call = the largest
  * iter_end - iter_begin the caller will pass).  philox_momenta = 0 (replay tapes, or a full cov_p,
- * which takes the per-chain kernel at every D > 128) sizes for those runs.  0 if unsupported.
+ * whose momenta the kernels draw in place, and whose lockstep blocks keep the inv(cov_p) products
+ * of their chains) sizes for those runs.  0 if unsupported.
  * hmc_nuts_workspace_size(D, n, d_max): enough for any call (iters_per_call 32, either kind). */
 int64_t hmc_nuts_workspace_size_ex(int32_t D, int64_t n_chains, int32_t d_max, int32_t iters_per_call,
                                    int32_t philox_momenta);
@@ -211,10 +212,11 @@ int64_t hmc_nuts_workspace_size(int32_t D, int64_t n_chains, int32_t d_max);
  * full cov_p (minv_full) at any D:
  *   D <= 128              the 16-chain MFMA tree kernel (hmc_nuts.hip; a full cov_p adds its
  *                         momentum and kinetic products on the same tiles);
- *   128 < D <= 320        diagonal cov_p: 16 chains per block in lockstep sharing one MFMA GEMM per
- *                         leapfrog (hmc_nuts_lock.hip);
- *   otherwise (D > 320, or a full cov_p at any D > 128) one wave per chain (hmc_nuts_big.hip;
- *                         a full cov_p as three GEMVs per leapfrog).
+ *   128 < D <= 320        16 chains per block in lockstep sharing one MFMA GEMM per leapfrog
+ *                         (hmc_nuts_lock.hip; a full cov_p adds the inv(cov_p) and Cholesky
+ *                         products as block GEMMs on the same fragments, round 6);
+ *   otherwise (D > 320)   one wave per chain (hmc_nuts_big.hip; a full cov_p as three GEMVs per
+ *                         leapfrog).
  * `workspace` (hmc_nuts_workspace_size bytes, or hmc_nuts_workspace_size_ex sized for the calls
  * made) must be zeroed before the first call of a run and kept between calls; hmc_nuts_iters_ws
  * also takes the workspace's size and refuses (HMC_EINVAL) a call that needs more.  Counters:

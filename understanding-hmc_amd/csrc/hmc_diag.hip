@@ -625,10 +625,14 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
   const int r = (local / a.G) * 8 + (id & 7), g = local % a.G;
   const Src& s = a.s;
   const int n = s.n, D = s.D, P = a.P, PK = a.PK;
-  // (PAIR: two staged groups per pair of barriers in two LDS buffers, measured 48.1 -> 50.5 ms at
-  // c4's halves; a second staging buffer two groups ahead: 48.1 -> 48.3 ms.  Neither is kept.)
-  constexpr bool PAIR = false;
-  constexpr int NBUF = PAIR ? 2 : 1;
+  // PIPE (n <= 144, where two sample buffers fit beside the other workgroup's): the staged group
+  // g + 1 is written to the other LDS buffer while group g's matrix work runs from registers, and
+  // group g + 1's operands are read into registers right after the group's one barrier -- no LDS
+  // wait in front of the MFMAs and one barrier per group instead of two (c4's halves: 45.6 -> see
+  // DESIGN.md §3.5).  (Two staged groups per pair of barriers: 48.1 -> 50.5 ms; a second
+  // staging register set two groups ahead: 48.1 -> 48.3 ms.  Neither is kept.)
+  constexpr bool PIPE = NTM <= 10;
+  constexpr int NBUF = PIPE ? 2 : 1;
   constexpr bool SQR_LDS = NTM > 10;               // the sq rows live in LDS (else in registers)
   const int SB = 4 * PK;
   double* const x0l = lds + NBUF * SB;
@@ -639,14 +643,12 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
   for (int i = tid; i < NBUF * (SB + kMfmaSer) + kMfmaSlack + (SQR_LDS ? kMfmaSer * kSqStride : 0); i += kMfmaThreads)
     lds[i] = 0.0;
   // staging role: wave = chain sk of the group, lane = (dim sw, row phase rho); rows rho + 16 i
-  const int sk = wv, sw = lane & 3, rho = lane >> 2;
+  // (sk wave-uniform in an SGPR: the chain's base offset is scalar arithmetic)
+  const int sk = uni(wv), sw = lane & 3, rho = lane >> 2;
   const int sd = g * kMfmaDims + sw;
-  // staged rows of a chain group: two buffers, so that a group's loads are issued two groups
-  // ahead of their LDS stores (one group of matrix work did not cover the HBM latency); the
-  // largest instance (NTM = 14) has no registers left for the second and keeps one group ahead
-  constexpr bool PF2 = PAIR;
-  double xsa[kRows], xsb[PF2 ? kRows : 1];
-  double x0a = 0.0, x0b = 0.0;
+  // staged rows of the next chain group (loads in flight under a group of matrix work)
+  double xsa[kRows];
+  double x0a = 0.0;
   // buffer loads based at the group's first split chain (uniform): one 32-bit lane offset (host-
   // checked below kLagOOB) plus 16 i rows (in the vector offset: the range check covers it); the
   // buffer ends with the view's last sample, so lanes past the range or the dims (offset kLagOOB)
@@ -665,19 +667,21 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
     for (int i = 0; i < kRows; ++i)
       xs[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lo + 16 * i * rowb, 0, 0));
   };
-  auto stage_store = [&](int nn, const double (&xs)[kRows], double x0s, int buf) {
+  // x0l holds x0 - S_d of each staged series (0 for chains past the range: their rows are zeros,
+  // so their moments add nothing)
+  const double Ssd = sd < D ? s.x[s.base + sd] : 0.0;
+  auto stage_store = [&](int nn, const double (&xs)[kRows], double x0s, int buf, bool valid) {
     double* dst = lds + buf * SB + sk * PK + sw * P + 16 + rho;
 #pragma unroll
     for (int i = 0; i < kRows; ++i) {
       if (i < kQAll || 16 * i + 15 < nn) dst[16 * i] = xs[i] - x0s;      // whole 16-row phase
       else if (16 * i < nn && rho + 16 * i < nn) dst[16 * i] = xs[i] - x0s;   // rows >= n stay zero
     }
-    if (rho == 0) x0l[buf * kMfmaSer + sk * 4 + sw] = x0s;
+    if (rho == 0) x0l[buf * kMfmaSer + sk * 4 + sw] = valid ? x0s - Ssd : 0.0;
   };
   // matrix role: wave wv = dimension d; lane = (chain k = lane >> 4, t' or s = lane & 15)
-  const int d = g * kMfmaDims + wv;
+  const int d = g * kMfmaDims + sk;
   const int k = lane >> 4, c16 = lane & 15;
-  const double Sd = d < D ? s.x[s.base + d] : 0.0;
   typedef double v4d __attribute__((ext_vector_type(4)));
   v4d acc[NTM];
 #pragma unroll
@@ -693,15 +697,42 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
   const int NT = a.NT;
   const double dn = n;
   const double rn = 1.0 / dn, rn1 = 1.0 / (dn - 1.0);
-  if (jlo < jhi) stage_load(jlo, xsa, x0a);
-  if constexpr (PF2) {
-    if (jlo + 4 < jhi) stage_load(jlo + 4, xsb, x0b);
-  }
+  // split moments, four groups at a time: after the row scans a group's totals (chain k: lane
+  // 16 k + 15) are parked by one DPP row_shl:4 per value (lanes 3, 7, 11 take the previous three
+  // groups' totals; lanes 12-15 the new ones), and the std/mean arithmetic runs once per four
+  // groups on lanes 3, 7, 11, 15 of each row (the other lanes' results are never read)
+  double pk1 = 0.0, pk2 = 0.0, pkx = 0.0;
+  int gi = 0;                                     // groups parked (wave-uniform)
+  auto park = [](double b, double v) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(v), __double2loint(b), 0x104, 0xF, 0x7, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(v), __double2hiint(b), 0x104, 0xF, 0x7, false);
+    return __hiloint2double(hi, lo);
+  };
+  auto flush = [&]() {
+    const double mm2 = pk2 - pk1 * (pk1 * rn);
+    a_std += sqrt(mm2 > 0.0 ? mm2 * rn1 : 0.0);
+    const double e = pkx + pk1 * rn;
+    a_m += e;
+    a_m2 = __builtin_fma(e, e, a_m2);
+  };
+  // the matrix operands of a group: A slices q = 0 .. NTM (rows 16 (q - 1) + 15 + t') and the B
+  // column of every anchor step (PIPE; else one step ahead, read inside matrix)
+  double sl[NTM + 1], bb[PIPE ? kNB : 1];
+  auto ops_ptr = [&](int buf) {
+    int zo = buf * SB + k * PK + wv * P + 16;     // (an opaque integer offset keeps sr an LDS pointer)
+    asm volatile("" : "+v"(zo));
+    return (const double*)(lds + zo);
+  };
+  auto read_ops = [&](int buf) {
+    const double* sr = ops_ptr(buf);
+#pragma unroll
+    for (int q = 0; q <= NTM; ++q) sl[q] = sr[16 * (q - 1) + 15 + c16];
+#pragma unroll
+    for (int bi = 0; bi < (PIPE ? kNB : 1); ++bi) bb[bi] = sr[16 * bi + 15 - c16];
+  };
   auto matrix = [&](int64_t jg, int nn, int buf) {
     if (d < D) {
-      int zo = buf * SB + k * PK + wv * P + 16;   // (an opaque integer offset keeps sr an LDS pointer)
-      asm volatile("" : "+v"(zo));
-      const double* sr = lds + zo;
+      const double* sr = ops_ptr(buf);
       // Anchor steps b = 16 bi + 15 (anchors b - 15 .. b: step 0 starts at anchor 0).  Every
       // product of tile ti (T = 16 (ti - 1)) at step bi pairs an anchor with row b + T + t' >=
       // 16 (bi + ti) - 1, so the tile meets a row below n only while 16 (bi + ti) <= n:
@@ -716,14 +747,14 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
 #ifdef HMC_MFMA_EDGE44
       const int e4 = ((nn & 15) >> 2) + 1;        // row groups of the edge tiles (4: a whole tile)
 #endif
-      double sl[NTM + 1];
-#pragma unroll
-      for (int q = 0; q <= NTM; ++q) sl[q] = sr[16 * (q - 1) + 15 + c16];
-      double bcur = sr[15 - c16];
+      if constexpr (!PIPE) read_ops(buf);
+      double bcur = bb[0];
       auto bstep = [&](auto bi_c) {
         constexpr int bi = decltype(bi_c)::value;
         const int tl = min(NT - 1, vt - bi);
-        const double bnx = bi + 1 < kNB ? sr[16 * (bi + 1) + 15 - c16] : 0.0;
+        double bnx = 0.0;
+        if constexpr (PIPE) bnx = bi + 1 < kNB ? bb[bi + 1 < kNB ? bi + 1 : 0] : 0.0;
+        else bnx = bi + 1 < kNB ? sr[16 * (bi + 1) + 15 - c16] : 0.0;
         auto tile = [&](auto ti_c) {
           constexpr int ti = decltype(ti_c)::value;
           if constexpr (bi + ti <= NTM) {
@@ -781,40 +812,73 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
         if constexpr (SQR) sqr[q] = __builtin_fma(y, y, sqr[q]);
         else if (q <= kQAll || q <= qn) sqa[16 * q + c16] = __builtin_fma(y, y, sv[q]);   // sq row 16 q + t' - 1
       }
-#pragma unroll
-      for (int m = 1; m < 16; m <<= 1) {
-        ps1 += __shfl_xor(ps1, m, 64);
-        ps2 += __shfl_xor(ps2, m, 64);
-      }
-      if (jg + k < jhi) {
-        const double mm2 = ps2 - ps1 * (ps1 * rn);
-        a_std += sqrt(mm2 > 0.0 ? mm2 * rn1 : 0.0);
-        const double e = (x0l[buf * kMfmaSer + k * 4 + wv] - Sd) + ps1 * rn;
-        a_m += e;
-        a_m2 = __builtin_fma(e, e, a_m2);
-      }
+      // the 16 row phases of chain k summed by a DPP row_shr scan: the total lands in the row's
+      // lane 15 (other lanes keep partial sums, accumulate into moments that are never read)
+      ps1 += dpp_u<0x111>(ps1);
+      ps2 += dpp_u<0x111>(ps2);
+      ps1 += dpp_u<0x112>(ps1);
+      ps2 += dpp_u<0x112>(ps2);
+      ps1 += dpp_u<0x114>(ps1);
+      ps2 += dpp_u<0x114>(ps2);
+      ps1 += dpp_u<0x118>(ps1);
+      ps2 += dpp_u<0x118>(ps2);
+      pk1 = park(pk1, ps1);
+      pk2 = park(pk2, ps2);
+      pkx = park(pkx, x0l[buf * kMfmaSer + k * 4 + wv]);
+      if ((gi & 3) == 3) flush();
+      ++gi;
     }
   };
-  for (int64_t jg = jlo; jg < jhi; jg += 4 * NBUF) {
-    int nn = n;                                   // opaque per group: bounds recomputed, not hoisted
-    asm volatile("" : "+s"(nn));
-#ifndef HMC_MFMA_DEV_NOSTAGE                      // dev timing variant: matrix work on stale LDS
-    __syncthreads();                              // the previous groups' slices are read
-    stage_store(nn, xsa, x0a, 0);
-    if constexpr (PAIR) {
-      if (jg + 4 < jhi) stage_store(nn, xsb, x0b, 1);
+  if (jlo < jhi) stage_load(jlo, xsa, x0a);
+  if constexpr (PIPE) {
+    // group jg in buffer buf: its operands are in registers when the iteration starts; the group
+    // jg + 4 is stored into buf ^ 1 (last read before the previous iteration's barrier) and read
+    // back after this iteration's barrier; the loads of group jg + 8 are issued before the matrix
+    // work and waited for before the barrier
+    if (jlo < jhi) {
+      __syncthreads();                            // the zeroed LDS
+      stage_store(n, xsa, x0a, 0, jlo + sk < jhi);
+      if (jlo + 4 < jhi) stage_load(jlo + 4, xsa, x0a);
+      __syncthreads();
+      if (d < D) read_ops(0);
     }
-    __syncthreads();
-    // the next groups' rows in flight under this pair's matrix work
-    if (jg + 4 * NBUF < jhi) stage_load(jg + 4 * NBUF, xsa, x0a);
-    if constexpr (PAIR) {
-      if (jg + 12 < jhi) stage_load(jg + 12, xsb, x0b);
+    int buf = 0;
+    for (int64_t jg = jlo; jg < jhi; jg += 4) {
+      int nn = n;                                 // opaque per group: bounds recomputed, not hoisted
+      asm volatile("" : "+s"(nn));
+      if (jg + 4 < jhi) {
+        stage_store(nn, xsa, x0a, buf ^ 1, jg + 4 + sk < jhi);
+        if (jg + 8 < jhi) stage_load(jg + 8, xsa, x0a);
+      }
+      matrix(jg, nn, buf);
+      // the loads just issued land before the barrier: the workgroups that read one row's 128-B
+      // lines stay in step and share them in L2.  FETCH_SIZE at c4's halves: 2.5x the samples
+      // without this wait (44.9 ms), 1.3x with it (43.2 ms); loads three groups ahead in two
+      // register sets with a wait for the older set: 2.0x, 44.1 ms
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();                            // group jg + 4 stored, group jg read
+      buf ^= 1;
+      if (jg + 4 < jhi && d < D) read_ops(buf);
     }
-#endif
-    matrix(jg, nn, 0);
-    if constexpr (PAIR) {
-      if (jg + 4 < jhi) matrix(jg + 4, nn, 1);
+  } else {
+    for (int64_t jg = jlo; jg < jhi; jg += 4) {
+      int nn = n;                                 // opaque per group: bounds recomputed, not hoisted
+      asm volatile("" : "+s"(nn));
+      __syncthreads();                            // the previous group's slices are read
+      stage_store(nn, xsa, x0a, 0, jg + sk < jhi);
+      __syncthreads();
+      if (jg + 4 < jhi) stage_load(jg + 4, xsa, x0a);   // in flight under this group's matrix work
+      matrix(jg, nn, 0);
     }
+  }
+  if (d < D && (gi & 3) != 0) {                   // the last groups: zero-padded to four
+    while ((gi & 3) != 0) {
+      pk1 = park(pk1, 0.0);
+      pk2 = park(pk2, 0.0);
+      pkx = park(pkx, 0.0);
+      ++gi;
+    }
+    flush();
   }
   // partial of this wave: tiles (entry t' * 16 + s), sq rows (summed over the 4 chain lanes; LDS
   // entry i holds row i - 1), moments
@@ -843,13 +907,17 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
       out[kMfmaNT * 256 + row] = v;
     }
   }
-  a_std += __shfl_xor(a_std, 16, 64);
-  a_std += __shfl_xor(a_std, 32, 64);
-  a_m += __shfl_xor(a_m, 16, 64);
-  a_m += __shfl_xor(a_m, 32, 64);
-  a_m2 += __shfl_xor(a_m2, 16, 64);
-  a_m2 += __shfl_xor(a_m2, 32, 64);
-  if (lane == 0) {
+  // moments: lanes 3, 7, 11, 15 of each row (the parked slots)
+  auto slots = [&](double v) {
+    v = (c16 & 3) == 3 ? v : 0.0;
+#pragma unroll
+    for (int m = 4; m < 64; m <<= 1) v += __shfl_xor(v, m, 64);
+    return v;
+  };
+  a_std = slots(a_std);
+  a_m = slots(a_m);
+  a_m2 = slots(a_m2);
+  if (lane == 63) {
     out[kMfmaNT * 256 + 256] = a_std;
     out[kMfmaNT * 256 + 257] = a_m;
     out[kMfmaNT * 256 + 258] = a_m2;
@@ -1265,9 +1333,11 @@ bool mfma_ok(const Src& s, int T) {
 
 // the samples, x0, the slack for the read-ahead past the last series, the sq rows
 size_t mfma_lds(const MfmaArgs& a) {
-  // k_conv_mfma<NTM <= 10> (n <= 144) keeps the sq rows in registers: no LDS for them
+  // k_conv_mfma<NTM <= 10> (n <= 144) keeps the sq rows in registers (no LDS for them) and
+  // double-buffers the samples and x0 (PIPE)
   const bool small = a.s.n <= 16 * 9;
-  return (size_t)(4 * a.PK + kMfmaSer + kMfmaSlack + (small ? 0 : kMfmaSer * kSqStride)) * sizeof(double);
+  const size_t buf = (size_t)(4 * a.PK + kMfmaSer);
+  return ((small ? 2 : 1) * buf + kMfmaSlack + (small ? 0 : kMfmaSer * kSqStride)) * sizeof(double);
 }
 
 int64_t mfma_work(const MfmaArgs& a) {
