@@ -1,5 +1,7 @@
 """C-ABI boundary checks that need no GPU: libhmc.so loads, exports every function
-include/hmc.h declares, and the ctypes struct mirrors match the C layouts."""
+include/hmc.h declares, the ctypes struct mirrors match the C layouts, and every entry that takes
+caller-sized device scratch refuses (HMC_EINVAL, before any launch) a buffer recorded as too small
+through its sized form or hmc_workspace_register (round 6)."""
 import ctypes
 import os
 import re

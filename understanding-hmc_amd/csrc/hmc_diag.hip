@@ -932,6 +932,12 @@ __global__ __launch_bounds__(256) void k_mfma_ranges(MfmaArgs a, const double* _
   const int d = (int)(i / kMfmaPW), e = (int)(i - (int64_t)d * kMfmaPW);
   const int g = d / kMfmaDims, w = d - g * kMfmaDims;
   double acc = 0.0;
+  // entries k_mfma_dims never reads (tiles past NT, sq rows past n): not summed (half the reads
+  // at n = 99, 8 of 16 tiles)
+  if ((e >= a.NT * 256 && e < kMfmaNT * 256) || (e >= kMfmaNT * 256 + a.s.n && e < kMfmaNT * 256 + 256)) {
+    red[i] = 0.0;
+    return;
+  }
   for (int r = 0; r < a.R; ++r) {
     const int id = ((r >> 3) * a.G + g) * 8 + (r & 7);   // inverse of k_conv_mfma's block map
     acc += partial[((int64_t)id * kMfmaDims + w) * kMfmaPW + e];
