@@ -604,8 +604,17 @@ struct MfmaArgs {
   int64_t per;      // split chains per range (a multiple of 4)
 };
 
+// W3: the small instance (NTM = 8, c4's halves) at three waves per SIMD (168 VGPRs: the B column
+// read a step ahead instead of up front; three workgroups' double buffers in 141 KB of LDS):
+// 41.40 -> 41.07 ms per c4 half (same box, alternating runs); more waves hide little here, the
+// pass is not latency-bound the way that would
+#ifndef HMC_MFMA_W2
+constexpr bool kMfmaW3 = true;
+#else
+constexpr bool kMfmaW3 = false;
+#endif
 template <int NTM>
-__global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_mfma(MfmaArgs a,
+__global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu((kMfmaW3 && NTM <= 8) ? 3 : 2, (kMfmaW3 && NTM <= 8) ? 3 : 2))) void k_conv_mfma(MfmaArgs a,
                                                                                              double* partial) {
   // capacity of this instance: NTM tiles, NTM - 1 anchor steps, n <= 16 (NTM - 1)
   constexpr int kNB = NTM - 1, kRows = NTM - 1;
@@ -717,7 +726,8 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
   };
   // the matrix operands of a group: A slices q = 0 .. NTM (rows 16 (q - 1) + 15 + t') and the B
   // column of every anchor step (PIPE; else one step ahead, read inside matrix)
-  double sl[NTM + 1], bb[PIPE ? kNB : 1];
+  constexpr bool BBALL = PIPE && !(kMfmaW3 && NTM <= 8);   // every step's B column up front
+  double sl[NTM + 1], bb[BBALL ? kNB : 1];
   auto ops_ptr = [&](int buf) {
     int zo = buf * SB + k * PK + wv * P + 16;     // (an opaque integer offset keeps sr an LDS pointer)
     asm volatile("" : "+v"(zo));
@@ -728,7 +738,7 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
 #pragma unroll
     for (int q = 0; q <= NTM; ++q) sl[q] = sr[16 * (q - 1) + 15 + c16];
 #pragma unroll
-    for (int bi = 0; bi < (PIPE ? kNB : 1); ++bi) bb[bi] = sr[16 * bi + 15 - c16];
+    for (int bi = 0; bi < (BBALL ? kNB : 1); ++bi) bb[bi] = sr[16 * bi + 15 - c16];
   };
   auto matrix = [&](int64_t jg, int nn, int buf) {
     if (d < D) {
@@ -753,7 +763,7 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu(2,
         constexpr int bi = decltype(bi_c)::value;
         const int tl = min(NT - 1, vt - bi);
         double bnx = 0.0;
-        if constexpr (PIPE) bnx = bi + 1 < kNB ? bb[bi + 1 < kNB ? bi + 1 : 0] : 0.0;
+        if constexpr (BBALL) bnx = bi + 1 < kNB ? bb[bi + 1 < kNB ? bi + 1 : 0] : 0.0;
         else bnx = bi + 1 < kNB ? sr[16 * (bi + 1) + 15 - c16] : 0.0;
         auto tile = [&](auto ti_c) {
           constexpr int ti = decltype(ti_c)::value;
@@ -1307,7 +1317,8 @@ MfmaArgs mfma_args(const Src& s) {
   a.G = (s.D + kMfmaDims - 1) / kMfmaDims;
   const int64_t m2 = n_series(s);
   const int64_t groups = (m2 + 3) / 4;
-  const int cus = device_cus() * 2;              // workgroups resident at a time (2 waves per SIMD)
+  // workgroups resident at a time (2 waves per SIMD; 3 for the W3 build's small instances)
+  const int cus = device_cus() * ((kMfmaW3 && n <= 16 * 7) ? 3 : 2);
   int best = 8;
   double best_eff = -1.0;
   for (int x = 1; x <= 64; ++x) {

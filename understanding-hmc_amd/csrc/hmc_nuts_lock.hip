@@ -158,11 +158,16 @@ __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom 
   auto wsum = [&](double s) { return wave_sum_dpp(s); };
 
   // g = P x; MASS: kv = inv_cov_p g (the kick), and the tree ends keep kv in their g slot
-  double q[J], p[J], g[J], kv[MASS ? J : 1], u[MASS ? J : 1];
+  // (MASS: the gradient and inv_cov_p p are step-local -- their energy terms are summed as they are
+  // gathered -- so only kv is carried between steps: 20 VGPRs fewer at J = 5)
+  double q[J], p[J], g[MASS ? 1 : J], kv[MASS ? J : 1];
+  double maha_l = 0.0, kin_l = 0.0;                 // MASS: this step's energy partials (lane, d order)
 #pragma unroll
-  for (int j = 0; j < J; ++j) q[j] = p[j] = g[j] = 0.0;
+  for (int j = 0; j < J; ++j) q[j] = p[j] = 0.0;
 #pragma unroll
-  for (int j = 0; j < (MASS ? J : 1); ++j) kv[j] = u[j] = 0.0;
+  for (int j = 0; j < (MASS ? 1 : J); ++j) g[j] = 0.0;
+#pragma unroll
+  for (int j = 0; j < (MASS ? J : 1); ++j) kv[j] = 0.0;
   int state = LS_FETCH;
   int64_t c = 0;
   uint64_t gc = 0;
@@ -203,14 +208,14 @@ __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom 
   };
   // E = V + K = 0.5 (logc + (q - q0).g + p.(minv p))  (samplers.py:811-823)
   auto energy = [&]() {
+    if constexpr (MASS) return 0.5 * (a.logc + (wsum(maha_l) + wsum(kin_l)));   // p . (inv_cov_p p)
     double maha = 0.0, kin = 0.0;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const int dd = lane + 64 * j;
       if (dd < D) {
         maha += (q[j] - dq0(j)) * g[j];
-        if constexpr (MASS) kin += p[j] * u[j];                 // p . (inv_cov_p p)
-        else kin += p[j] * (dminv(j) * p[j]);
+        kin += p[j] * (dminv(j) * p[j]);
       }
     }
     return 0.5 * (a.logc + (wsum(maha) + wsum(kin)));
@@ -365,9 +370,22 @@ __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom 
     };
     gemm(rpf);
     __syncthreads();
-    if (busy) gather(g);                                    // g = P (q - q0)
+    if constexpr (!MASS) {
+      if (busy) gather(g);                                  // g = P (q - q0)
+    }
     if constexpr (MASS) {
-      product(rmf, g, kv, busy, busy);                      // the kick inv_cov_p dVdq (:835-837)
+      double gl[J];                                         // g = P (q - q0), this step only
+      maha_l = 0.0;
+      kin_l = 0.0;
+      if (busy) {
+        gather(gl);
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+          const int dd = lane + 64 * j;
+          if (dd < D) maha_l += (q[j] - dq0(j)) * gl[j];
+        }
+      }
+      product(rmf, gl, kv, busy, busy);                     // the kick inv_cov_p dVdq (:835-837)
       if (state == LS_GRAD) {                               // iteration start: p ~ N(0, cov_p) (:565, :829)
 #pragma unroll
         for (int j = 0; j < J; ++j) {
@@ -399,7 +417,26 @@ __global__ __launch_bounds__(64 * kLockW) void k_nuts_lock(RandArgs a, LockGeom 
           }
         }
       }
-      product(rmf, p, u, busy, busy);                       // inv_cov_p p for K (:823)
+      // inv_cov_p p for K (:823), summed against p as its rows are gathered
+      if (busy) {
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+          const int dd = lane + 64 * j;
+          if (dd < 4 * KS) sX[dd * kLockXS + w] = dd < D ? p[j] : 0.0;
+        }
+      }
+      __syncthreads();
+      gemm(rmf);
+      __syncthreads();
+      if (busy) {
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+          const int dd = lane + 64 * j;
+          double sacc = 0.0;
+          for (int t = 0; t < gcnt[j]; ++t) sacc += sSeg[(gseg[j] + t) * (16 * kLockXS) + (dd & 15) * kLockXS + w];
+          if (dd < D) kin_l += p[j] * sacc;
+        }
+      }
     }
 
     // ================= post-gradient
