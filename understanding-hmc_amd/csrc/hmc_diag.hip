@@ -1317,8 +1317,11 @@ MfmaArgs mfma_args(const Src& s) {
   a.G = (s.D + kMfmaDims - 1) / kMfmaDims;
   const int64_t m2 = n_series(s);
   const int64_t groups = (m2 + 3) / 4;
-  // workgroups resident at a time (2 waves per SIMD; 3 for the W3 build's small instances)
-  const int cus = device_cus() * ((kMfmaW3 && n <= 16 * 7) ? 3 : 2);
+  // workgroups resident at a time, as two per CU for every instance: the range count must not
+  // depend on n, because diag_conv_work sizes the partials at n = kMfmaMinN for any n (a W3-aware
+  // count, 3 per CU below n = 113, made a c3 pass at n = 200 write past a work buffer sized at a
+  // different R)
+  const int cus = device_cus() * 2;
   int best = 8;
   double best_eff = -1.0;
   for (int x = 1; x <= 64; ++x) {
@@ -1361,8 +1364,20 @@ int64_t mfma_work(const MfmaArgs& a) {
   return (int64_t)a.R * a.G * kMfmaDims * kMfmaPW + (int64_t)a.s.D * kMfmaPW;
 }
 
+// the matrix-core partials' bound that diag_conv_work reserves (the geometry at n = kMfmaMinN,
+// either series layout): every launch checks its own geometry against it
+int64_t mfma_work_bound(int64_t n_chains, int D) {
+  int64_t w = 0;
+  for (int halves = 1; halves <= 2; ++halves) {
+    Src s{nullptr, 0, 0, 0, n_chains, kMfmaMinN, D, halves};
+    w = std::max(w, mfma_work(mfma_args(s)));
+  }
+  return w;
+}
+
 hipError_t launch_conv_mfma(const Src& s, int nlag, double* work, double* out, hipStream_t st) {
   const MfmaArgs a = mfma_args(s);
+  if (mfma_work(a) > mfma_work_bound(s.n_chains, s.D)) return hipErrorInvalidValue;   // never past the work
   double* partial = work;
   double* red = work + (int64_t)a.R * a.G * kMfmaDims * kMfmaPW;
   const unsigned grid = (unsigned)(a.R * a.G);
@@ -1509,12 +1524,7 @@ int64_t diag_conv_work(int64_t n_chains, int D, int T) {
   int64_t w = lag_work_bound(n_chains, D, T, 1);
   // a complete pass of split chains of kMfmaMinN .. T + 2 samples may take the matrix cores (their
   // geometry depends on the chains and dims only)
-  if (T + 2 >= kMfmaMinN) {
-    for (int halves = 1; halves <= 2; ++halves) {   // stored split chains, or streaming halves
-      Src s{nullptr, 0, 0, 0, n_chains, kMfmaMinN, D, halves};
-      w = std::max(w, mfma_work(mfma_args(s)));
-    }
-  }
+  if (T + 2 >= kMfmaMinN) w = std::max(w, mfma_work_bound(n_chains, D));   // stored split chains or halves
   return w;
 }
 
