@@ -58,6 +58,13 @@ CASES = [
     (3, 193, 13, 0, 1, 1, 94),         # n = 96 (the smallest), D = 13: a partial dim group; 6 split
                                        # chains: one full chain group of 4 and a ragged one
     (3, 257, 13, 0, 1, 1, 126),        # n = 128, the same groups
+    # the static-triangle instances of 97 <= n <= 111 (k_conv_mfma<8, E4, 6>): each anchor step's
+    # last tile as E4 = 1, 2, 3 4x4x4 MFMAs (n % 16 = 1, 5, 9), whole (n % 16 = 14); n = 112 runtime
+    (3, 195, 13, 0, 1, 1, 95),         # n = 97, E4 = 1
+    (5, 203, 21, 0, 1, 1, 99),         # n = 101, E4 = 2, a partial dim group, a ragged chain group
+    (3, 211, 13, 0, 1, 1, 103),        # n = 105, E4 = 3
+    (6, 221, 17, 0, 1, 1, 108),        # n = 110, static triangle, whole last tiles
+    (3, 225, 13, 0, 1, 1, 110),        # n = 112 (16 | n): the runtime-bound instance
     (2, 417, 100, 0, 1, 1, 206),       # n = 208 (the largest): every tile and anchor step
     (2, 481, 100, 0, 1, 1, 238),       # n = 240: past the matrix-core range (VALU lag kernel)
     (5, 300, 101, 1, 1, 1, 200),       # n = 149, a D = 100 view with odd row stride; tmax beyond n - 1

@@ -613,7 +613,11 @@ constexpr bool kMfmaW3 = true;
 #else
 constexpr bool kMfmaW3 = false;
 #endif
-template <int NTM>
+// VT >= 0 (NTM = 8 only, 97 <= n <= 111): the tile bound n / 16 = VT and NT = NTM are compile-time,
+// so the triangle is static (no per-MFMA branches, no merges of accumulator tuples).  E4 (1..3,
+// with VT): n % 16 < 12, and each anchor step's last tile runs as E4 v_mfma_f64_4x4x4 on the row
+// groups that meet rows below n (a quarter of a 16x16x4's cycles each) instead of a whole tile.
+template <int NTM, int E4 = 0, int VT = -1>
 __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu((kMfmaW3 && NTM <= 8) ? 3 : 2, (kMfmaW3 && NTM <= 8) ? 3 : 2))) void k_conv_mfma(MfmaArgs a,
                                                                                              double* partial) {
   // capacity of this instance: NTM tiles, NTM - 1 anchor steps, n <= 16 (NTM - 1)
@@ -754,9 +758,6 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu((k
       // slices q = 0 .. NTM are read once, up front, into registers; B of the next step is read a
       // step ahead.  Reads past row n + 29 land in the next series or the LDS slack, feed no MFMA.
       const int vt = nn >> 4;                     // tiles ti <= vt - bi meet rows below n
-#ifdef HMC_MFMA_EDGE44
-      const int e4 = ((nn & 15) >> 2) + 1;        // row groups of the edge tiles (4: a whole tile)
-#endif
       if constexpr (!PIPE) read_ops(buf);
       double bcur = bb[0];
       auto bstep = [&](auto bi_c) {
@@ -768,19 +769,15 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu((k
         auto tile = [&](auto ti_c) {
           constexpr int ti = decltype(ti_c)::value;
           if constexpr (bi + ti <= NTM) {
-#ifdef HMC_MFMA_EDGE44
-            if (ti < tl || (ti == tl && e4 == 4)) {
-#else
-            if (ti <= tl) {
-#endif
+            constexpr int tls = VT - bi;          // (VT >= 0: the static bound)
+            if (VT >= 0 ? (E4 > 0 ? ti < tls : ti <= tls) : ti <= tl) {
 #ifdef HMC_MFMA_DEV_NOLDS                         // dev timing variant: no LDS operands
               acc[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(dn, dn, acc[ti], 0, 0, 0);
 #else
               acc[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(sl[bi + ti], bcur, acc[ti], 0, 0, 0);
 #endif
             }
-#ifdef HMC_MFMA_EDGE44
-            else if (ti == tl) {
+            else if (VT >= 0 && E4 > 0 && ti == tls) {
               // the step's edge tile: rows 16 (bi + ti) - 1 + t' < n only for t' <= n % 16, i.e.
               // accumulator components g < e4 (rows 4 g .. 4 g + 3).  Each takes one
               // v_mfma_f64_4x4x4f64 (a quarter of the 16x16x4 cost): its four blocks share the A
@@ -788,14 +785,13 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu((k
               // (lane (k, s)), and its result lane (i, blk, j) is entry (4 g + i, 4 blk + j) --
               // the lane and component g where the 16x16x4 layout keeps that entry.
 #pragma unroll
-              for (int g = 0; g < 3; ++g) {
-                if (g < e4) {
+              for (int g = 0; g < (E4 > 0 ? E4 : 1); ++g) {
+                if constexpr (E4 > 0) {
                   const double a4 = sr[16 * (bi + ti - 1) + 15 + 4 * g + (c16 & 3)];
                   acc[ti][g] = __builtin_amdgcn_mfma_f64_4x4x4f64(a4, bcur, acc[ti][g], 0, 0, 0);
                 }
               }
             }
-#endif
           }
         };
         static_for<NTM>(tile);
@@ -1382,7 +1378,14 @@ hipError_t launch_conv_mfma(const Src& s, int nlag, double* work, double* out, h
   double* red = work + (int64_t)a.R * a.G * kMfmaDims * kMfmaPW;
   const unsigned grid = (unsigned)(a.R * a.G);
   if (s.n <= 16 * 5) k_conv_mfma<6><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
-  else if (s.n <= 16 * 7) k_conv_mfma<8><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
+  else if (s.n <= 16 * 7) {
+    const int e4 = ((s.n & 15) >> 2) + 1;         // row groups of the steps' last tiles
+    if (s.n < 97 || s.n > 111) k_conv_mfma<8><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
+    else if (e4 == 1) k_conv_mfma<8, 1, 6><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
+    else if (e4 == 2) k_conv_mfma<8, 2, 6><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
+    else if (e4 == 3) k_conv_mfma<8, 3, 6><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
+    else k_conv_mfma<8, 0, 6><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
+  }
   else if (s.n <= 16 * 9) k_conv_mfma<10><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
   else if (s.n <= 16 * 11) k_conv_mfma<12><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
   else k_conv_mfma<14><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
