@@ -861,7 +861,9 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu((k
       // lines stay in step and share them in L2.  FETCH_SIZE at c4's halves: 2.5x the samples
       // without this wait (44.9 ms), 1.3x with it (43.2 ms); loads three groups ahead in two
       // register sets with a wait for the older set: 2.0x, 44.1 ms
+#ifndef HMC_MFMA_NO_THROTTLE
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
       __syncthreads();                            // group jg + 4 stored, group jg read
       buf ^= 1;
       if (jg + 4 < jhi && d < D) read_ops(buf);
