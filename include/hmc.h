@@ -181,7 +181,9 @@ hmc_status hmc_random_iters_ws(const hmc_target* t, const hmc_kinetic* k, const 
 
 /* Record the size of a scratch buffer (hmc_state.order or a NUTS workspace) for the unsized entry
  * points: a later call that would need more than `bytes` returns HMC_EINVAL instead of writing past
- * the end.  bytes = 0 forgets the buffer.  Host-side bookkeeping only (no device access). */
+ * the end.  bytes = 0 forgets the buffer; a record stays until the pointer is registered again, so
+ * register (or use a sized form) again after reallocating.  Host-side bookkeeping only (no device
+ * access). */
 hmc_status hmc_workspace_register(const void* workspace, int64_t bytes);
 
 /* Bytes of the optional hmc_state.order scratch for hmc_random_iters on this target

@@ -65,6 +65,11 @@ CASES = [
     (3, 211, 13, 0, 1, 1, 103),        # n = 105, E4 = 3
     (6, 221, 17, 0, 1, 1, 108),        # n = 110, static triangle, whole last tiles
     (3, 225, 13, 0, 1, 1, 110),        # n = 112 (16 | n): the runtime-bound instance
+    # k_conv_mfma<14, E4, 12> (193 <= n <= 207): E4 = 1, 2, 3 (c3's n = 200), whole last tiles
+    (3, 387, 13, 0, 1, 1, 191),        # n = 193, E4 = 1
+    (5, 395, 21, 0, 1, 1, 195),        # n = 197, E4 = 2, a partial dim group, a ragged chain group
+    (3, 401, 13, 0, 1, 1, 198),        # n = 200, E4 = 3
+    (3, 413, 13, 0, 1, 1, 204),        # n = 206, static triangle, whole last tiles
     (2, 417, 100, 0, 1, 1, 206),       # n = 208 (the largest): every tile and anchor step
     (2, 481, 100, 0, 1, 1, 238),       # n = 240: past the matrix-core range (VALU lag kernel)
     (5, 300, 101, 1, 1, 1, 200),       # n = 149, a D = 100 view with odd row stride; tmax beyond n - 1

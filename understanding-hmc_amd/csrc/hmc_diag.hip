@@ -613,7 +613,8 @@ constexpr bool kMfmaW3 = true;
 #else
 constexpr bool kMfmaW3 = false;
 #endif
-// VT >= 0 (NTM = 8 only, 97 <= n <= 111): the tile bound n / 16 = VT and NT = NTM are compile-time,
+// VT >= 0 (NTM = 8 with 97 <= n <= 111, NTM = 14 with 193 <= n <= 207: VT = NTM - 2 = n / 16 and
+// NT = NTM): the tile bound and the tile count are compile-time,
 // so the triangle is static (no per-MFMA branches, no merges of accumulator tuples).  E4 (1..3,
 // with VT): n % 16 < 12, and each anchor step's last tile runs as E4 v_mfma_f64_4x4x4 on the row
 // groups that meet rows below n (a quarter of a 16x16x4's cycles each) instead of a whole tile.
@@ -1390,7 +1391,14 @@ hipError_t launch_conv_mfma(const Src& s, int nlag, double* work, double* out, h
   }
   else if (s.n <= 16 * 9) k_conv_mfma<10><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
   else if (s.n <= 16 * 11) k_conv_mfma<12><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
-  else k_conv_mfma<14><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
+  else if (s.n < 193 || s.n > 207) k_conv_mfma<14><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
+  else {                                          // c3's n = 200: E4 = 3
+    const int e4 = ((s.n & 15) >> 2) + 1;
+    if (e4 == 1) k_conv_mfma<14, 1, 12><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
+    else if (e4 == 2) k_conv_mfma<14, 2, 12><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
+    else if (e4 == 3) k_conv_mfma<14, 3, 12><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
+    else k_conv_mfma<14, 0, 12><<<grid, kMfmaThreads, mfma_lds(a), st>>>(a, partial);
+  }
   if (hipError_t e = hipGetLastError()) return e;
   const int64_t nr = (int64_t)s.D * kMfmaPW;
   k_mfma_ranges<<<(unsigned)((nr + 255) / 256), 256, 0, st>>>(a, partial, red);
