@@ -40,8 +40,10 @@ constexpr int kNutsWaves = HMC_NUTS_WAVES;
 // next block waits behind the whole grid's current one; its last kNutsTail iterations run as one unit
 // per (chain, iteration), which keeps the launch's tail at one tree per slot.  kNutsBlock 1 gives the
 // per-tree units only.
+// (round 6, with the release/acquire hand-off: blocks of 12 beat 8 by 1.0%, 10 and 14 lost 0.3% and
+// 3%, 16 lost 2.5%: profiles/r06s_nuts_block_ab.txt)
 #ifndef HMC_NUTS_BLOCK
-#define HMC_NUTS_BLOCK 8
+#define HMC_NUTS_BLOCK 12
 #endif
 #ifndef HMC_NUTS_TAIL
 #define HMC_NUTS_TAIL 4
