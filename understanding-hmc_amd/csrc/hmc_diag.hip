@@ -654,6 +654,9 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu((k
   const int64_t m2 = n_series(s);
   const int64_t jlo = (int64_t)r * a.per;
   const int64_t jhi = jlo + a.per < m2 ? jlo + a.per : m2;
+  // split chains of this range (< 2^31), the group loop in 32-bit offsets o from jlo: its bounds
+  // are scalar compares (int64 compares of wave-uniform values run on the VALU)
+  const int nrem = jhi > jlo ? (int)(jhi - jlo) : 0;
   for (int i = tid; i < NBUF * (SB + kMfmaSer) + kMfmaSlack + (SQR_LDS ? kMfmaSer * kSqStride : 0); i += kMfmaThreads)
     lds[i] = 0.0;
   // staging role: wave = chain sk of the group, lane = (dim sw, row phase rho); rows rho + 16 i
@@ -669,12 +672,12 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu((k
   // and rows past the last chain's end read zeros (y = 0 - 0)
   const int rowb = (int)(s.sample_stride * 8);
   const double* const vend = split_ptr(s, m2 - 1, n - 1) + D;
-  auto stage_load = [&](int64_t jg, double (&xs)[kRows], double& x0s) {
-    const int64_t j = jg + sk;
+  auto stage_load = [&](int o, double (&xs)[kRows], double& x0s) {
+    const int64_t jg = jlo + o, j = jg + sk;
     const double* b = uni(split_ptr(s, jg, 0));
     const int64_t span = (vend - b) * 8;
     const int nrec = span < kLagOOB ? (int)span : kLagOOB;
-    const int lo = (sd < D && j < jhi) ? (int)((split_ptr(s, j, 0) - b) + sd) * 8 + rho * rowb : kLagOOB + 64;
+    const int lo = (sd < D && o + sk < nrem) ? (int)((split_ptr(s, j, 0) - b) + sd) * 8 + rho * rowb : kLagOOB + 64;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(b), 0, nrec, 0x00020000);
     x0s = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, lo - rho * rowb, 0, 0));
 #pragma unroll
@@ -745,7 +748,7 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu((k
 #pragma unroll
     for (int bi = 0; bi < (BBALL ? kNB : 1); ++bi) bb[bi] = sr[16 * bi + 15 - c16];
   };
-  auto matrix = [&](int64_t jg, int nn, int buf) {
+  auto matrix = [&](int nn, int buf) {
     if (d < D) {
       const double* sr = ops_ptr(buf);
       // Anchor steps b = 16 bi + 15 (anchors b - 15 .. b: step 0 starts at anchor 0).  Every
@@ -802,7 +805,7 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu((k
       // split moments of chain k and the sq rows from the slices q = 0 .. kRows (rows
       // 16 (q - 1) + 15 + t': every row once; row -1 and rows >= n are zeros or masked), the 16 row
       // phases reduced in a fixed xor order
-      double ps1 = 0.0, ps2 = 0.0;
+      double ps1, ps2;
       double sv[kRows + 1];
 #pragma unroll
       for (int q = 0; q <= kRows; ++q) sv[q] = SQR ? 0.0 : sqa[16 * q + c16];
@@ -814,8 +817,13 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu((k
         // a guarded update per slice that the compiler turned into six v_cndmask per slice
         double y = sl[q];
         if (q > kQAll) y = q <= qn ? y : 0.0;
-        ps1 += y;
-        ps2 = __builtin_fma(y, y, ps2);
+        if (q == 0) {                             // (no add to a zero start)
+          ps1 = y;
+          ps2 = y * y;
+        } else {
+          ps1 += y;
+          ps2 = __builtin_fma(y, y, ps2);
+        }
         if constexpr (SQR) sqr[q] = __builtin_fma(y, y, sqr[q]);
         else if (q <= kQAll || q <= qn) sqa[16 * q + c16] = __builtin_fma(y, y, sv[q]);   // sq row 16 q + t' - 1
       }
@@ -836,28 +844,28 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu((k
       ++gi;
     }
   };
-  if (jlo < jhi) stage_load(jlo, xsa, x0a);
+  if (nrem > 0) stage_load(0, xsa, x0a);
   if constexpr (PIPE) {
     // group jg in buffer buf: its operands are in registers when the iteration starts; the group
     // jg + 4 is stored into buf ^ 1 (last read before the previous iteration's barrier) and read
     // back after this iteration's barrier; the loads of group jg + 8 are issued before the matrix
     // work and waited for before the barrier
-    if (jlo < jhi) {
+    if (nrem > 0) {
       __syncthreads();                            // the zeroed LDS
-      stage_store(n, xsa, x0a, 0, jlo + sk < jhi);
-      if (jlo + 4 < jhi) stage_load(jlo + 4, xsa, x0a);
+      stage_store(n, xsa, x0a, 0, sk < nrem);
+      if (4 < nrem) stage_load(4, xsa, x0a);
       __syncthreads();
       if (d < D) read_ops(0);
     }
     int buf = 0;
-    for (int64_t jg = jlo; jg < jhi; jg += 4) {
+    for (int o = 0; o < nrem; o += 4) {
       int nn = n;                                 // opaque per group: bounds recomputed, not hoisted
       asm volatile("" : "+s"(nn));
-      if (jg + 4 < jhi) {
-        stage_store(nn, xsa, x0a, buf ^ 1, jg + 4 + sk < jhi);
-        if (jg + 8 < jhi) stage_load(jg + 8, xsa, x0a);
+      if (o + 4 < nrem) {
+        stage_store(nn, xsa, x0a, buf ^ 1, o + 4 + sk < nrem);
+        if (o + 8 < nrem) stage_load(o + 8, xsa, x0a);
       }
-      matrix(jg, nn, buf);
+      matrix(nn, buf);
       // the loads just issued land before the barrier: the workgroups that read one row's 128-B
       // lines stay in step and share them in L2.  FETCH_SIZE at c4's halves: 2.5x the samples
       // without this wait (44.9 ms), 1.3x with it (43.2 ms); loads three groups ahead in two
@@ -867,17 +875,17 @@ __global__ __launch_bounds__(kMfmaThreads) __attribute__((amdgpu_waves_per_eu((k
 #endif
       __syncthreads();                            // group jg + 4 stored, group jg read
       buf ^= 1;
-      if (jg + 4 < jhi && d < D) read_ops(buf);
+      if (o + 4 < nrem && d < D) read_ops(buf);
     }
   } else {
-    for (int64_t jg = jlo; jg < jhi; jg += 4) {
+    for (int o = 0; o < nrem; o += 4) {
       int nn = n;                                 // opaque per group: bounds recomputed, not hoisted
       asm volatile("" : "+s"(nn));
       __syncthreads();                            // the previous group's slices are read
-      stage_store(nn, xsa, x0a, 0, jg + sk < jhi);
+      stage_store(nn, xsa, x0a, 0, o + sk < nrem);
       __syncthreads();
-      if (jg + 4 < jhi) stage_load(jg + 4, xsa, x0a);   // in flight under this group's matrix work
-      matrix(jg, nn, 0);
+      if (o + 4 < nrem) stage_load(o + 4, xsa, x0a);    // in flight under this group's matrix work
+      matrix(nn, 0);
     }
   }
   if (d < D && (gi & 3) != 0) {                   // the last groups: zero-padded to four
